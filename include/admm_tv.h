@@ -1,0 +1,96 @@
+/* admm_tv.h -- C ABI of the MI355X (gfx950) ADMM-TV deconvolution library.
+ *
+ * This is the drop-in boundary for the hot path of georgegrosu1/torch-admm-deconv
+ * ("admmtor").  The reference is pure Python/PyTorch, so its "FFI" for this path
+ * is the Python call  admmtor.eops.deconv.fft_admm_tv(xin, lmbd, rho, kern, iso,
+ * maxit)  (/root/reference/src/admmtor/eops/deconv.py:35-40) and the module
+ * ADMMDeconv.forward (/root/reference/src/admmtor/elayers/admmdeconv.py:63-64).
+ * The Python mirror in torch-admm-deconv_amd/admmtor binds the entry points below
+ * through ctypes (see INTEGRATION.md for the binding a maintainer would add).
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers (hipMalloc / PyTorch caching allocator),
+ *    fp32, C-contiguous NCHW.  lambda / rho are device scalars, read on the GPU
+ *    (no host synchronisation, graph-capturable).
+ *  - `stream` is a hipStream_t passed as void* (0 = legacy default stream).
+ *    Every call is asynchronous with respect to the host, like an ATen op.
+ *  - The caller owns input, output and workspace.  The workspace must be at
+ *    least admm_tv_workspace_size() bytes and 256-byte aligned.
+ *  - Return value: 0 on success, a negative ADMM_TV_E* code otherwise.  Error
+ *    classes mirror the reference's exceptions: the Python
+ *    wrapper raises ValueError for ADMM_TV_EINVAL_RANK and RuntimeError
+ *    otherwise.
+ */
+#ifndef ADMM_TV_H
+#define ADMM_TV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADMM_TV_ABI_VERSION 1
+
+enum {
+    ADMM_TV_OK = 0,
+    ADMM_TV_EINVAL = -1,        /* null pointer / negative sizes / maxit < 0       */
+    ADMM_TV_EUNSUPPORTED = -2,  /* H, W not a supported power of two (see below)    */
+    ADMM_TV_ENONSQUARE = -3,    /* kh != kw  (reference: RuntimeError, deconv.py:90-96) */
+    ADMM_TV_EWORKSPACE = -4,    /* workspace too small / misaligned                 */
+    ADMM_TV_EHIP = -5,          /* a HIP runtime call or kernel launch failed       */
+    ADMM_TV_EKERNEL = -6        /* PSF larger than the image                        */
+};
+
+/* Problem descriptor.  Replaces the shapes/flags of fft_admm_tv's arguments
+ * (deconv.py:35-42): xin (B,C,H,W), kern (1,1,kh,kw) or empty (kh = kw = 0),
+ * iso (False = soft/anisotropic shrink, True = block shrink with the per-pixel
+ * norm over batch AND channel, deconv.py:19-24), maxit (>= 0).
+ * Supported on the device path: H in {16..4096}, W in {16..2048}, powers of two. */
+typedef struct admm_tv_desc {
+    int64_t B, C, H, W;
+    int32_t kh, kw;
+    int32_t iso;
+    int32_t maxit;
+} admm_tv_desc;
+
+/* ABI version (ADMM_TV_ABI_VERSION). */
+int admm_tv_abi_version(void);
+
+/* 1 if (H, W) can run on the HIP path, 0 otherwise. */
+int admm_tv_supported(int64_t H, int64_t W);
+
+/* Workspace bytes needed by admm_tv_forward for `desc`. */
+int admm_tv_workspace_size(const admm_tv_desc* desc, size_t* bytes);
+
+/* The whole solver: replaces fft_admm_tv(xin, lmbd, rho, kern, iso, maxit)
+ * (deconv.py:35-117).  Computes b = H_t(xin) once, freq_c from the PSF spectrum
+ * and rho, then `maxit` ADMM iterations (two fused passes each, three for iso),
+ * and writes the final x to `out` (B,C,H,W).  maxit == 0 writes zeros.
+ * kern may be NULL iff kh == kw == 0 (pure TV denoising, sigma = 1).            */
+int admm_tv_forward(const admm_tv_desc* desc, const float* xin, const float* kern,
+                    const float* lambda_dev, const float* rho_dev, float* out,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* b = H_t(xin): the reference's circular PSF "adjoint" (a centred circular
+ * CONVOLUTION, deconv.py:86-101), via the same FFT passes.  Exposed for tests. */
+int admm_tv_psf_transpose(const admm_tv_desc* desc, const float* xin, const float* kern,
+                          float* out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Per-kernel timing of the iteration passes (HIP events on the launch stream),
+ * used by bench.py for the roofline line.  enable != 0 starts recording;
+ * read() synchronises on the recorded events and returns totals since the last
+ * reset: ms[k], count[k] for k = 0 pass A (row pass), 1 pass B (column pass),
+ * 2 iso norm pass, 3 setup.                                                    */
+int admm_tv_profile_enable(int enable);
+int admm_tv_profile_reset(void);
+int admm_tv_profile_read(double* ms4, int64_t* count4);
+
+/* Human-readable text for the last error on this thread. */
+const char* admm_tv_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ADMM_TV_H */

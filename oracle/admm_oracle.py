@@ -1,0 +1,245 @@
+"""CPU oracle for the ADMM-TV deconvolution hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product package (``admmtor``) may
+import, call or execute this file.  Only ``tests/``, ``__graft_entry__.smoke()``
+and the ``cpu_baseline`` leg of ``bench.py`` use it, and only as the checker /
+the timed CPU baseline, never as the thing measured or shipped.
+
+It restates, in two independent ways, the algorithm of the reference solver
+``fft_admm_tv`` (``/root/reference/src/admmtor/eops/deconv.py:35-117``):
+
+* :func:`solve_spatial` follows the reference's operator sequence: every linear
+  operator is a circular pad followed by a depthwise ``conv2d`` and the PSF
+  adjoint ``H_t(xin)`` is re-evaluated inside the loop, exactly as the reference
+  does (deconv.py:98-104).  It is the ``cpu_baseline`` ("port") timed by
+  ``bench.py``: same op mix, same cost profile as the reference on the same cores.
+* :func:`solve_fourier` is the Fourier-domain restatement the HIP path
+  implements (``b = H_t(xin)`` once, differences by ``roll``, the Wiener factor
+  applied to the 2-D real spectrum).  It runs in any float dtype; in fp64 it
+  agrees with the reference's fp64 output to ~1e-14.
+
+Parity pinning: both restatements are checked against golden vectors produced
+by importing the reference itself in the build container
+(``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``; test
+``tests/test_oracle_golden.py``).
+
+Semantics restated (all circular, per (b,c) plane; line numbers in deconv.py):
+
+* ``Dx a = a[i,j] - a[i,j-1]``, ``Dy a = a[i,j] - a[i-1,j]``          (:51-52, 74-78)
+* ``Dx_t a = a[i,j] - a[i,j+1]``, ``Dy_t a = a[i,j] - a[i+1,j]``      (:80-84)
+* ``H_t`` = circular *convolution* with the PSF anchored at
+  ``c = ceil((k-1)/2)`` (pads ``(floor, ceil)`` on each side, flipped kernel,
+  cross-correlation) -- not the adjoint for non-centrosymmetric PSFs  (:86-101)
+* ``freq_c = 1 / (|sigma|^2 + rho (|Dx^|^2 + |Dy^|^2))``, ``sigma = rfft2(kern, s=(H,W))`` (:46-57)
+* soft shrink ``sign(a) max(|a|-tau, 0)``; block shrink
+  ``max(1 - tau/(sqrt(sum_{b,c} a^2 + 1e-15) + 1e-15), 0) a`` (norm over dims 0,1)  (:15-24)
+* ``tau = lmbd / rho``; ``x = z = u = 0`` initially; returns the last ``x``  (:44, 61-67, 103-117)
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable
+
+import torch
+import torch.nn.functional as F
+
+__all__ = [
+    "psf_conv_pads",
+    "apply_psf_transpose",
+    "shrink_soft",
+    "shrink_block",
+    "wiener_factor",
+    "solve_spatial",
+    "solve_fourier",
+    "rel_l2",
+]
+
+
+# --------------------------------------------------------------------------
+# small helpers
+# --------------------------------------------------------------------------
+def rel_l2(a: torch.Tensor, b: torch.Tensor) -> float:
+    """||a-b|| / ||b|| in fp64."""
+    a = torch.as_tensor(a).double()
+    b = torch.as_tensor(b).double()
+    den = torch.linalg.vector_norm(b).item()
+    num = torch.linalg.vector_norm(a - b).item()
+    return num / den if den > 0 else num
+
+
+def psf_conv_pads(k: int) -> tuple[int, int]:
+    """(before, after) circular padding of H_t for a k-tap axis (deconv.py:90-96).
+
+    The reference pads ``floor((k-1)/2)`` before and ``ceil((k-1)/2)`` after and
+    cross-correlates with the flipped PSF, i.e. convolves with the PSF anchored
+    at ``ceil((k-1)/2)``.
+    """
+    return (k - 1) // 2, k // 2  # floor((k-1)/2), ceil((k-1)/2)
+
+
+def _dw(stencil, C: int, like: torch.Tensor) -> torch.Tensor:
+    w = torch.tensor(stencil, dtype=like.dtype, device=like.device).reshape(1, 1, 2, 2)
+    return w.expand(C, 1, 2, 2).contiguous()
+
+
+def _circ_dwconv(a: torch.Tensor, w: torch.Tensor, pad: tuple[int, int, int, int]) -> torch.Tensor:
+    return F.conv2d(F.pad(a, pad, mode="circular"), w, groups=a.shape[1])
+
+
+def apply_psf_transpose(x: torch.Tensor, kern: torch.Tensor) -> torch.Tensor:
+    """H_t(x) as the reference evaluates it: circular pad + depthwise conv with the flipped PSF."""
+    if kern.numel() == 0:
+        return x
+    kh, kw = kern.shape[-2:]
+    if kh != kw:
+        raise RuntimeError("non-square PSF: the reference's H_t pads are swapped and fail (deconv.py:90-96)")
+    C = x.shape[1]
+    lo, hi = psf_conv_pads(kh)
+    w = kern.flip((2, 3)).expand(C, 1, kh, kw).contiguous()
+    return F.conv2d(F.pad(x, (lo, hi, lo, hi), mode="circular"), w, groups=C)
+
+
+def shrink_soft(a: torch.Tensor, tau) -> torch.Tensor:
+    """sign(a) * max(|a| - tau, 0)  (deconv.py:15-16)."""
+    return torch.sign(a) * torch.clamp_min(torch.abs(a) - tau, 0.0)
+
+
+def shrink_block(a: torch.Tensor, tau) -> torch.Tensor:
+    """max(1 - tau / (||a||_(B,C) + 1e-15), 0) * a with the norm over dims (0,1) (deconv.py:19-24)."""
+    nrm = torch.sqrt(torch.sum(a * a, dim=(0, 1)) + 1e-15)
+    return torch.clamp_min(1.0 - tau / (nrm + 1e-15), 0.0) * a
+
+
+def wiener_factor(H: int, W: int, kern: torch.Tensor, rho, dtype=torch.float64) -> torch.Tensor:
+    """freq_c on the (H, W//2+1) half-plane (deconv.py:46-57), computed in ``dtype``."""
+    ky = torch.arange(H, dtype=torch.float64).reshape(H, 1)
+    kx = torch.arange(W // 2 + 1, dtype=torch.float64).reshape(1, -1)
+    lap = (2.0 - 2.0 * torch.cos(2 * math.pi * kx / W)) + (2.0 - 2.0 * torch.cos(2 * math.pi * ky / H))
+    if kern.numel() == 0:
+        s2 = torch.ones((H, W // 2 + 1), dtype=torch.float64)
+    else:
+        sig = torch.fft.rfftn(kern.detach().double().reshape(kern.shape[-2:]), s=(H, W))
+        s2 = sig.real ** 2 + sig.imag ** 2
+    rho_d = torch.as_tensor(rho, dtype=torch.float64).reshape(())
+    return (1.0 / (s2 + rho_d * lap)).to(dtype)
+
+
+# --------------------------------------------------------------------------
+# restatement 1: the reference's operator sequence (timed CPU baseline)
+# --------------------------------------------------------------------------
+def solve_spatial(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool = False,
+                  maxit: int = 100, iters_cb: Callable[[int, torch.Tensor], None] | None = None) -> torch.Tensor:
+    """ADMM-TV with the reference's op mix: pad+depthwise-conv operators, FFT x-update.
+
+    Differentiable w.r.t. xin, lmbd, rho and kern through ordinary autograd.
+    """
+    if xin.dim() != 4:
+        raise ValueError("expected a 4-D (B,C,H,W) input")
+    B, C, H, W = xin.shape
+    dt = xin.dtype
+    lmbd = torch.as_tensor(lmbd, dtype=dt)
+    rho = torch.as_tensor(rho, dtype=dt)
+    tau = lmbd / rho
+
+    # Wiener factor in the working dtype, built like deconv.py:46-57
+    if kern.numel() == 0:
+        s2 = torch.ones((), dtype=dt)
+    else:
+        sig = torch.fft.rfftn(kern, s=(H, W), dim=(2, 3))
+        s2 = sig.real ** 2 + sig.imag ** 2
+    kx = torch.arange(W // 2 + 1, dtype=dt)
+    ky = torch.arange(H, dtype=dt).reshape(H, 1)
+    lap = (2 - 2 * torch.cos(2 * math.pi * kx / W)) + (2 - 2 * torch.cos(2 * math.pi * ky / H))
+    fc = 1.0 / (s2 + rho * lap)
+
+    wdx = _dw([[0, 0], [-1, 1]], C, xin)
+    wdy = _dw([[0, -1], [0, 1]], C, xin)
+    wdxt = _dw([[1, -1], [0, 0]], C, xin)
+    wdyt = _dw([[1, 0], [-1, 0]], C, xin)
+    back = (1, 0, 1, 0)
+    fwd = (0, 1, 0, 1)
+    shrink = shrink_block if iso else shrink_soft
+
+    x = torch.zeros_like(xin)
+    zx = torch.zeros_like(xin)
+    zy = torch.zeros_like(xin)
+    ux = torch.zeros_like(xin)
+    uy = torch.zeros_like(xin)
+    for it in range(int(maxit)):
+        rhs = apply_psf_transpose(xin, kern) + rho * (
+            _circ_dwconv(zx - ux, wdxt, fwd) + _circ_dwconv(zy - uy, wdyt, fwd))
+        x = torch.fft.irfftn(fc * torch.fft.rfftn(rhs, dim=(2, 3)), s=(H, W), dim=(2, 3))
+        gx = _circ_dwconv(x, wdx, back)
+        gy = _circ_dwconv(x, wdy, back)
+        zx = shrink(gx + ux, tau)
+        zy = shrink(gy + uy, tau)
+        ux = ux + gx - zx
+        uy = uy + gy - zy
+        if iters_cb is not None:
+            iters_cb(it, x)
+    return x
+
+
+# --------------------------------------------------------------------------
+# restatement 2: Fourier-domain form (what the HIP path computes)
+# --------------------------------------------------------------------------
+def _psf_centered_spectrum(kern: torch.Tensor, H: int, W: int) -> torch.Tensor:
+    """Spectrum of the circular convolution that H_t applies (PSF anchored at ceil((k-1)/2))."""
+    k = kern.shape[-1]
+    c = k // 2
+    sig = torch.fft.rfftn(kern.reshape(kern.shape[-2:]), s=(H, W))
+    ky = torch.arange(H, dtype=torch.float64).reshape(H, 1)
+    kx = torch.arange(W // 2 + 1, dtype=torch.float64).reshape(1, -1)
+    ph = torch.exp(2j * math.pi * c * (ky / H + kx / W)).to(sig.dtype)
+    return sig * ph
+
+
+def solve_fourier(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool = False,
+                  maxit: int = 100, return_state: bool = False):
+    """Fourier-domain restatement (b once, roll differences) in xin's dtype."""
+    B, C, H, W = xin.shape
+    dt = xin.dtype
+    lmbd = torch.as_tensor(lmbd, dtype=dt)
+    rho = torch.as_tensor(rho, dtype=dt)
+    tau = lmbd / rho
+    if kern.numel() == 0:
+        b = xin
+    else:
+        if kern.shape[-1] != kern.shape[-2]:
+            raise RuntimeError("non-square PSF")
+        b = torch.fft.irfftn(torch.fft.rfftn(xin, dim=(2, 3)) * _psf_centered_spectrum(kern.to(dt), H, W),
+                             s=(H, W), dim=(2, 3))
+    fc = wiener_factor(H, W, kern, rho, dtype=torch.float64).to(dt)
+
+    def Dx(a):
+        return a - torch.roll(a, 1, dims=3)
+
+    def Dy(a):
+        return a - torch.roll(a, 1, dims=2)
+
+    def DxT(a):
+        return a - torch.roll(a, -1, dims=3)
+
+    def DyT(a):
+        return a - torch.roll(a, -1, dims=2)
+
+    shrink = shrink_block if iso else shrink_soft
+    x = torch.zeros_like(xin)
+    ux = torch.zeros_like(xin)
+    uy = torch.zeros_like(xin)
+    wx = torch.zeros_like(xin)  # z - u
+    wy = torch.zeros_like(xin)
+    for _ in range(int(maxit)):
+        r = b + rho * (DxT(wx) + DyT(wy))
+        x = torch.fft.irfftn(fc * torch.fft.rfftn(r, dim=(2, 3)), s=(H, W), dim=(2, 3))
+        ax = Dx(x) + ux
+        ay = Dy(x) + uy
+        zx = shrink(ax, tau)
+        zy = shrink(ay, tau)
+        ux = ax - zx
+        uy = ay - zy
+        wx = zx - ux
+        wy = zy - uy
+    if return_state:
+        return x, dict(b=b, fc=fc, ux=ux, uy=uy)
+    return x

@@ -1,0 +1,197 @@
+"""Generate the golden parity fixtures by running the REFERENCE solver in this container.
+
+Run from the repo root (build container only; /root/reference does not exist on
+the GPU box, and nothing at test time reads it):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference's ``fft_admm_tv`` (``/root/reference/src/admmtor/eops/deconv.py:35-117``)
+is loaded straight from its source file (read-only; no bytecode is written) and
+run in fp64 and fp32 on inputs made by the build's own generator
+(``admmtor/synth.py``).  Each fixture stores inputs and outputs only (data, no
+reference code).  fp64 outputs of the larger fixtures are stored rounded to
+fp32 (relative rounding <= 6e-8, far below the 1e-5 parity gate).
+
+Fixture list:
+  g1_c1          C1 exact: 1x1x256^2, 9x9 Gaussian s=1.5, lam .01, rho .02, 30 it, aniso
+  g2_motion      reduced C2: 2x3x128^2, 15x15 one-sided motion PSF, 50 it, aniso + iso
+  g3_c3          reduced C3: 1x3x256^2, 21x21 Gaussian s=3, 100 it, aniso (+ 50 it)
+  g4_train_grad  train config: 2x3x64^2, no PSF, iso, 100 it, fp64 grads (xin, lam, rho)
+  g5_psf_grad    2x3x32^2, 5x5 random PSF, 20 it, fp64 grads incl. the PSF (aniso + iso)
+  g6_inter       1x1x64^2, 7x7 Gaussian: freq_c, b = H_t(xin), x after 1 and 2 iterations
+  g7_edges       maxit 0/1, odd 15x17 with an even 4x4 PSF, 32x32 no-PSF iso, 16x64
+  errors.json    exception class names the reference raises for the boundary error cases
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "torch-admm-deconv_amd"))
+from admmtor.synth import CONFIG_SEED, blurred_batch, make_psf  # noqa: E402
+
+REF_FILE = "/root/reference/src/admmtor/eops/deconv.py"
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def load_reference():
+    sys.dont_write_bytecode = True
+    spec = importlib.util.spec_from_file_location("_ref_deconv", REF_FILE)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def f32(t):
+    return t.detach().to(torch.float32).cpu().numpy()
+
+
+def f64(t):
+    return t.detach().to(torch.float64).cpu().numpy()
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def run_pair(ref, x32, psf32, lam, rho, iso, it):
+    o64 = ref.fft_admm_tv(x32.double(), lam, rho, psf32.double() if psf32.numel() else psf32.double(), iso, it)
+    o32 = ref.fft_admm_tv(x32, lam, rho, psf32, iso, it)
+    return o64, o32
+
+
+def main():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    ref = load_reference()
+    meta = {}
+
+    # ---- g1: C1 exact -------------------------------------------------------
+    psf = make_psf("gauss:1.5", 9)
+    x = blurred_batch(1, 1, 256, 256, psf, seed=CONFIG_SEED + 0)
+    o64, o32 = run_pair(ref, x, psf, 0.01, 0.02, False, 30)
+    np.savez_compressed(os.path.join(OUT, "g1_c1.npz"), x=f32(x), psf=f32(psf), lam=0.01, rho=0.02, iso=False,
+                        maxit=30, ref64=f32(o64), ref32=f32(o32))
+    meta["g1_c1"] = {"ref32_vs_ref64": rel(o32, o64)}
+
+    # ---- g2: reduced C2, motion PSF, aniso + iso ----------------------------
+    psf = make_psf("motion", 15)
+    x = blurred_batch(2, 3, 128, 128, psf, seed=CONFIG_SEED + 1)
+    oa64, oa32 = run_pair(ref, x, psf, 0.01, 0.02, False, 50)
+    oi64, oi32 = run_pair(ref, x, psf, 0.01, 0.02, True, 50)
+    np.savez_compressed(os.path.join(OUT, "g2_motion.npz"), x=f32(x), psf=f32(psf), lam=0.01, rho=0.02, maxit=50,
+                        ref64_aniso=f32(oa64), ref64_iso=f32(oi64))
+    meta["g2_motion"] = {"aniso_ref32_vs_ref64": rel(oa32, oa64), "iso_ref32_vs_ref64": rel(oi32, oi64)}
+
+    # ---- g3: reduced C3 ------------------------------------------------------
+    psf = make_psf("gauss:3", 21)
+    x = blurred_batch(1, 3, 256, 256, psf, seed=CONFIG_SEED + 2)
+    o64, o32 = run_pair(ref, x, psf, 0.01, 0.02, False, 100)
+    o64_50 = ref.fft_admm_tv(x.double(), 0.01, 0.02, psf.double(), False, 50)
+    np.savez_compressed(os.path.join(OUT, "g3_c3.npz"), x=f32(x), psf=f32(psf), lam=0.01, rho=0.02, maxit=100,
+                        ref64=f32(o64), ref64_it50=f32(o64_50))
+    meta["g3_c3"] = {"ref32_vs_ref64": rel(o32, o64)}
+
+    # ---- g4: train-config gradients (no PSF, iso, 100 it), fp64 --------------
+    x = blurred_batch(2, 3, 64, 64, torch.empty(0), seed=CONFIG_SEED + 4).double().requires_grad_(True)
+    lam = torch.tensor([0.05], dtype=torch.float64, requires_grad=True)
+    rho = torch.tensor([0.1], dtype=torch.float64, requires_grad=True)
+    out = ref.fft_admm_tv(x, lam, rho, torch.empty(0, dtype=torch.float64), True, 100)
+    g = torch.Generator().manual_seed(99)
+    cot = torch.randn(out.shape, generator=g, dtype=torch.float64)
+    gx, gl, gr = torch.autograd.grad(out, (x, lam, rho), cot)
+    np.savez_compressed(os.path.join(OUT, "g4_train_grad.npz"), x=f64(x), lam=f64(lam), rho=f64(rho), maxit=100,
+                        iso=True, out=f64(out), cot=f64(cot), gx=f64(gx), glam=f64(gl), grho=f64(gr))
+
+    # ---- g5: gradients with a PSF, incl. dPSF, fp64 --------------------------
+    psf = make_psf("random", 5).double()
+    x0 = blurred_batch(2, 3, 32, 32, psf.float(), seed=CONFIG_SEED + 5).double()
+    g5 = {"x": f64(x0), "psf": f64(psf), "lam": 0.02, "rho": 0.05, "maxit": 20}
+    for iso in (False, True):
+        x = x0.clone().requires_grad_(True)
+        k = psf.clone().requires_grad_(True)
+        lam = torch.tensor([0.02], dtype=torch.float64, requires_grad=True)
+        rho = torch.tensor([0.05], dtype=torch.float64, requires_grad=True)
+        out = ref.fft_admm_tv(x, lam, rho, k, iso, 20)
+        cot = torch.randn(out.shape, generator=torch.Generator().manual_seed(7), dtype=torch.float64)
+        gx, gl, gr, gk = torch.autograd.grad(out, (x, lam, rho, k), cot)
+        tag = "iso" if iso else "aniso"
+        g5.update({f"out_{tag}": f64(out), f"cot_{tag}": f64(cot), f"gx_{tag}": f64(gx), f"glam_{tag}": f64(gl),
+                   f"grho_{tag}": f64(gr), f"gpsf_{tag}": f64(gk)})
+    np.savez_compressed(os.path.join(OUT, "g5_psf_grad.npz"), **g5)
+
+    # ---- g6: intermediates ----------------------------------------------------
+    psf = make_psf("gauss:1.2", 7)
+    x = blurred_batch(1, 1, 64, 64, psf, seed=CONFIG_SEED + 6)
+    xd, pd = x.double(), psf.double()
+    sig = torch.fft.rfftn(pd, s=(64, 64), dim=(2, 3))
+    dxb = torch.tensor([[[[0, 0], [-1, 1]]]], dtype=torch.float64)
+    dyb = torch.tensor([[[[0, -1], [0, 1]]]], dtype=torch.float64)
+    lap = ref.torch_abs2(torch.fft.rfftn(dxb, s=(1, 1, 64, 64))) + ref.torch_abs2(torch.fft.rfftn(dyb, s=(1, 1, 64, 64)))
+    freq_c = 1 / (ref.torch_abs2(sig) + 0.02 * lap)
+    bt = ref.conv_circular(xd, pd.flip((2, 3)), (3, 3, 3, 3), 1)  # H_t for k=7 (pads 3/3)
+    x1 = ref.fft_admm_tv(xd, 0.01, 0.02, pd, False, 1)
+    x2 = ref.fft_admm_tv(xd, 0.01, 0.02, pd, False, 2)
+    np.savez_compressed(os.path.join(OUT, "g6_inter.npz"), x=f32(x), psf=f32(psf), lam=0.01, rho=0.02,
+                        freq_c=f64(freq_c).reshape(64, 33), b=f64(bt), x_it1=f64(x1), x_it2=f64(x2))
+
+    # ---- g7: edge cases --------------------------------------------------------
+    e = {}
+    psf = make_psf("gauss:1.5", 9)
+    x = blurred_batch(1, 2, 32, 32, psf, seed=CONFIG_SEED + 7)
+    e["m0_x"], e["m0_psf"] = f32(x), f32(psf)
+    e["m0_out"] = f64(ref.fft_admm_tv(x.double(), 0.01, 0.02, psf.double(), False, 0))
+    e["m1_out"] = f64(ref.fft_admm_tv(x.double(), 0.01, 0.02, psf.double(), False, 1))
+    psf4 = make_psf("random", 4)
+    xo = blurred_batch(1, 2, 15, 17, torch.empty(0), seed=CONFIG_SEED + 8)
+    e["odd_x"], e["odd_psf"] = f32(xo), f32(psf4)
+    e["odd_out"] = f64(ref.fft_admm_tv(xo.double(), 0.01, 0.02, psf4.double(), False, 20))
+    xn = blurred_batch(3, 2, 32, 32, torch.empty(0), seed=CONFIG_SEED + 9)
+    e["noPSF_iso_x"] = f32(xn)
+    e["noPSF_iso_out"] = f64(ref.fft_admm_tv(xn.double(), 0.03, 0.05, torch.empty(0, dtype=torch.float64), True, 40))
+    e["even4_x"] = f32(blurred_batch(2, 1, 32, 32, psf4, seed=CONFIG_SEED + 10))
+    e["even4_psf"] = f32(psf4)
+    e["even4_out"] = f64(ref.fft_admm_tv(torch.from_numpy(e["even4_x"]).double(), 0.01, 0.02, psf4.double(), False, 25))
+    xr = blurred_batch(2, 3, 16, 64, make_psf("motion", 5), seed=CONFIG_SEED + 11)
+    e["rect_x"], e["rect_psf"] = f32(xr), f32(make_psf("motion", 5))
+    e["rect_out_aniso"] = f64(ref.fft_admm_tv(xr.double(), 0.01, 0.02, make_psf("motion", 5).double(), False, 30))
+    e["rect_out_iso"] = f64(ref.fft_admm_tv(xr.double(), 0.01, 0.02, make_psf("motion", 5).double(), True, 30))
+    np.savez_compressed(os.path.join(OUT, "g7_edges.npz"), **e)
+
+    # ---- error behaviour of the reference boundary ------------------------------
+    errs = {}
+
+    def grab(name, fn):
+        try:
+            fn()
+            errs[name] = None
+        except Exception as ex:  # record the class only
+            errs[name] = type(ex).__name__
+
+    x4 = torch.rand(1, 1, 16, 16)
+    grab("input_3d", lambda: ref.fft_admm_tv(torch.rand(1, 16, 16), 0.01, 0.02, torch.empty(0), False, 2))
+    grab("input_5d", lambda: ref.fft_admm_tv(torch.rand(1, 1, 1, 16, 16), 0.01, 0.02, torch.empty(0), False, 2))
+    grab("kernel_nonsquare", lambda: ref.fft_admm_tv(x4, 0.01, 0.02, torch.rand(1, 1, 3, 5), False, 2))
+    grab("kernel_dtype_mismatch", lambda: ref.fft_admm_tv(x4, 0.01, 0.02, torch.rand(1, 1, 3, 3).double(), False, 2))
+    grab("input_bf16", lambda: ref.fft_admm_tv(x4.bfloat16(), 0.01, 0.02, torch.empty(0), False, 2))
+    grab("input_fp16", lambda: ref.fft_admm_tv(x4.half(), 0.01, 0.02, torch.empty(0), False, 2))
+    grab("kernel_2ch", lambda: ref.fft_admm_tv(torch.rand(1, 2, 16, 16), 0.01, 0.02, torch.rand(1, 2, 3, 3), False, 2))
+    grab("kernel_2d", lambda: ref.fft_admm_tv(x4, 0.01, 0.02, torch.rand(3, 3), False, 2))
+    grab("maxit_0_ok", lambda: ref.fft_admm_tv(x4, 0.01, 0.02, torch.empty(0), False, 0))
+    meta["errors"] = errs
+    with open(os.path.join(OUT, "errors.json"), "w") as f:
+        json.dump(errs, f, indent=1, sort_keys=True)
+    with open(os.path.join(OUT, "meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(json.dumps(meta, indent=1))
+
+
+if __name__ == "__main__":
+    main()

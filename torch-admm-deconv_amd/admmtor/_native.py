@@ -1,0 +1,136 @@
+"""ctypes binding of the MI355X C ABI (include/admm_tv.h -> admmtor/_lib/libadmm_tv.so).
+
+The shared library is the product: there is no CPU or PyTorch fallback.  If the
+library is missing or fails to load, every entry point raises loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libadmm_tv.so")
+
+ADMM_TV_OK = 0
+ADMM_TV_EINVAL = -1
+ADMM_TV_EUNSUPPORTED = -2
+ADMM_TV_ENONSQUARE = -3
+ADMM_TV_EWORKSPACE = -4
+ADMM_TV_EHIP = -5
+ADMM_TV_EKERNEL = -6
+
+# every symbol include/admm_tv.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED = (
+    "admm_tv_abi_version",
+    "admm_tv_supported",
+    "admm_tv_workspace_size",
+    "admm_tv_forward",
+    "admm_tv_psf_transpose",
+    "admm_tv_profile_enable",
+    "admm_tv_profile_reset",
+    "admm_tv_profile_read",
+    "admm_tv_last_error",
+)
+
+
+class AdmmTvDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int64),
+        ("C", ctypes.c_int64),
+        ("H", ctypes.c_int64),
+        ("W", ctypes.c_int64),
+        ("kh", ctypes.c_int32),
+        ("kw", ctypes.c_int32),
+        ("iso", ctypes.c_int32),
+        ("maxit", ctypes.c_int32),
+    ]
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"admm_tv native error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the native library; raises ImportError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(_LIB_PATH):
+            raise ImportError(
+                f"admmtor: the HIP library {_LIB_PATH} is missing. Build it with "
+                "`python __graft_entry__.py build` (or `make -C torch-admm-deconv_amd/csrc`). "
+                "There is no CPU fallback.")
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        dp = ctypes.POINTER(AdmmTvDesc)
+        L.admm_tv_abi_version.restype = ctypes.c_int
+        L.admm_tv_abi_version.argtypes = []
+        L.admm_tv_supported.restype = ctypes.c_int
+        L.admm_tv_supported.argtypes = [ctypes.c_int64, ctypes.c_int64]
+        L.admm_tv_workspace_size.restype = ctypes.c_int
+        L.admm_tv_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
+        L.admm_tv_forward.restype = ctypes.c_int
+        L.admm_tv_forward.argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp]
+        L.admm_tv_psf_transpose.restype = ctypes.c_int
+        L.admm_tv_psf_transpose.argtypes = [dp, vp, vp, vp, vp, sz, vp]
+        L.admm_tv_profile_enable.restype = ctypes.c_int
+        L.admm_tv_profile_enable.argtypes = [ctypes.c_int]
+        L.admm_tv_profile_reset.restype = ctypes.c_int
+        L.admm_tv_profile_reset.argtypes = []
+        L.admm_tv_profile_read.restype = ctypes.c_int
+        L.admm_tv_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+        L.admm_tv_last_error.restype = ctypes.c_char_p
+        L.admm_tv_last_error.argtypes = []
+        if L.admm_tv_abi_version() != 1:
+            raise ImportError("admmtor: native library ABI version mismatch")
+        _lib = L
+        return L
+
+
+def check(code: int) -> None:
+    if code != ADMM_TV_OK:
+        msg = load().admm_tv_last_error().decode(errors="replace")
+        raise NativeError(code, msg)
+
+
+def desc(B, C, H, W, k, iso, maxit) -> AdmmTvDesc:
+    return AdmmTvDesc(int(B), int(C), int(H), int(W), int(k), int(k), int(bool(iso)), int(maxit))
+
+
+def workspace_size(d: AdmmTvDesc) -> int:
+    n = ctypes.c_size_t(0)
+    check(load().admm_tv_workspace_size(ctypes.byref(d), ctypes.byref(n)))
+    return int(n.value)
+
+
+def supported(H: int, W: int) -> bool:
+    return bool(load().admm_tv_supported(int(H), int(W)))
+
+
+def profile_enable(on: bool) -> None:
+    check(load().admm_tv_profile_enable(1 if on else 0))
+
+
+def profile_reset() -> None:
+    check(load().admm_tv_profile_reset())
+
+
+def profile_read():
+    """-> (ms[4], count[4]) for pass A, pass B, iso norm, setup."""
+    ms = (ctypes.c_double * 4)()
+    n = (ctypes.c_int64 * 4)()
+    check(load().admm_tv_profile_read(ms, n))
+    return list(ms), list(n)

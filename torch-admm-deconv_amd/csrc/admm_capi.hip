@@ -1,0 +1,462 @@
+// admm_capi.hip -- host side of the MI355X ADMM-TV library: the C ABI declared in
+// include/admm_tv.h.  Orchestrates setup kernels and the per-iteration passes on
+// the caller's stream; no host synchronisation, no allocation (workspace is the
+// caller's), so the whole call is graph-capturable.
+//
+// Replaces the reference's Python loop  fft_admm_tv  (deconv.py:35-117): ~30 ATen
+// launches per iteration there, 2 fused kernels per iteration here (3 for iso).
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "admm_kernels.hpp"
+#include "admm_tv.h"
+
+using namespace admm;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+// ------------------------------------------------------------------ profiling
+struct ProfRec {
+    int kind;
+    hipEvent_t a, b;
+};
+struct Prof {
+    bool on = false;
+    std::vector<ProfRec> recs;
+    std::vector<hipEvent_t> pool;
+    double ms[4] = {0, 0, 0, 0};
+    int64_t n[4] = {0, 0, 0, 0};
+} g_prof;
+
+hipEvent_t prof_event() {
+    if (!g_prof.pool.empty()) {
+        hipEvent_t e = g_prof.pool.back();
+        g_prof.pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+struct ProfScope {
+    int kind;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(int k, hipStream_t st) : kind(k), s(st) {
+        if (g_prof.on) {
+            a = prof_event();
+            b = prof_event();
+            if (a && b) (void)hipEventRecord(a, s);
+        }
+    }
+    ~ProfScope() {
+        if (a && b) {
+            (void)hipEventRecord(b, s);
+            g_prof.recs.push_back({kind, a, b});
+        }
+    }
+};
+
+// ------------------------------------------------------------------ geometry
+bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
+
+bool supported_hw(int64_t H, int64_t W) {
+    return pow2(H) && pow2(W) && H >= 16 && H <= 4096 && W >= 16 && W <= 2048;
+}
+
+constexpr size_t kAlign = 256;
+size_t up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
+
+struct Layout {
+    size_t spec[2], u[4], b, fcT, mT, twW, twH, twHd, G, part, nsq, total;
+    int ngroups, ppg;
+};
+
+Layout make_layout(const admm_tv_desc& d) {
+    Layout L{};
+    const size_t P = (size_t)d.B * d.C, H = d.H, W = d.W, N = W / 2;
+    const size_t img = P * H * W * sizeof(float);
+    const int k = d.kh;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        size_t at = o;
+        o += up(bytes);
+        return at;
+    };
+    L.spec[0] = take(img);
+    L.spec[1] = take(img);
+    for (int i = 0; i < 4; ++i) L.u[i] = take(img);
+    L.b = k > 0 ? take(img) : 0;
+    L.fcT = take((N + 1) * H * sizeof(float));
+    L.mT = take((N + 1) * H * sizeof(cf));
+    L.twW = take(W * sizeof(cf));
+    L.twH = take(H * sizeof(cf));
+    L.twHd = take(H * sizeof(double2));
+    L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
+    if (d.iso) {
+        // plane groups for the iso norm pass: enough (group,row) items to fill the chip
+        int ppg = 8;
+        if ((size_t)P <= 8) ppg = (int)P;
+        L.ppg = ppg;
+        L.ngroups = (int)((P + ppg - 1) / ppg);
+        L.part = take((size_t)L.ngroups * 2 * H * W * sizeof(float));
+        L.nsq = take(2 * H * W * sizeof(float));
+    }
+    L.total = o;
+    return L;
+}
+
+int env_int(const char* name, int dflt) {
+    const char* s = std::getenv(name);
+    return s ? std::atoi(s) : dflt;
+}
+
+template <class T> T* at(void* ws, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(ws) + off); }
+
+#define HIPCHK(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) return fail(ADMM_TV_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class K> int set_lds(K kern, size_t bytes) {
+    if (bytes > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return fail(ADMM_TV_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+    }
+    return 0;
+}
+
+int launch_check(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ADMM_TV_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    return 0;
+}
+
+// ------------------------------------------------------------------ row-side ops (templated on N = W/2)
+template <int N> struct RowOps {
+    using G = RowKernelGeom<N>;
+    static unsigned blocks(long long items) { return (unsigned)((items + G::SG - 1) / G::SG); }
+
+    static int r2c(const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s) {
+        hipLaunchKernelGGL(k_row_r2c<N>, dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, img, spec, twW, rows);
+        return launch_check("k_row_r2c");
+    }
+    static int c2r(const cf* spec, float* img, const cf* twW, long long rows, hipStream_t s) {
+        hipLaunchKernelGGL(k_row_c2r<N>, dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, spec, img, twW, rows);
+        return launch_check("k_row_c2r");
+    }
+    static int pass_a(const PassAArgs& a, bool iso, bool first, hipStream_t s) {
+        const unsigned nb = blocks(a.nstrips);
+        if (iso) {
+            if (first)
+                hipLaunchKernelGGL((k_pass_a<N, true, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+            else
+                hipLaunchKernelGGL((k_pass_a<N, true, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        } else {
+            if (first)
+                hipLaunchKernelGGL((k_pass_a<N, false, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+            else
+                hipLaunchKernelGGL((k_pass_a<N, false, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        }
+        return launch_check("k_pass_a");
+    }
+    static int iso_norm(const IsoArgs& a, bool first, hipStream_t s) {
+        const unsigned nb = blocks(a.nitems);
+        if (first)
+            hipLaunchKernelGGL((k_iso_norm<N, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        else
+            hipLaunchKernelGGL((k_iso_norm<N, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        return launch_check("k_iso_norm");
+    }
+};
+
+template <class F> int with_row(int N, F&& f) {
+    switch (N) {
+        case 8: return f(RowOps<8>{});
+        case 16: return f(RowOps<16>{});
+        case 32: return f(RowOps<32>{});
+        case 64: return f(RowOps<64>{});
+        case 128: return f(RowOps<128>{});
+        case 256: return f(RowOps<256>{});
+        case 512: return f(RowOps<512>{});
+        case 1024: return f(RowOps<1024>{});
+        default: return fail(ADMM_TV_EUNSUPPORTED, "unsupported W");
+    }
+}
+
+// ------------------------------------------------------------------ column-side ops (templated on H, C)
+template <int H, int C> int pass_b_hc(cf* spec, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode,
+                                      hipStream_t s) {
+    using G = ColGeom<H, C>;
+    const int colblocks = N / C;
+    const dim3 grid((unsigned)((long long)P * colblocks));
+    if (mode == 0) {
+        if (int e = set_lds(k_pass_b<H, C, 0>, G::lds_bytes())) return e;
+        hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, fcT, mT, twH, N, colblocks);
+    } else {
+        if (int e = set_lds(k_pass_b<H, C, 1>, G::lds_bytes())) return e;
+        hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, fcT, mT, twH, N, colblocks);
+    }
+    return launch_check("k_pass_b");
+}
+
+template <int H> int pass_b_h(cf* spec, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode,
+                              hipStream_t s) {
+    constexpr int L = ColGeom<H, 1>::L;
+    if constexpr (L <= 64) {
+        int C = env_int("ADMM_PASSB_C", 16);
+        if (C > N) C = N;
+        if (C >= 16) return pass_b_hc<H, 16>(spec, fcT, mT, twH, N, P, mode, s);
+        return pass_b_hc<H, 8>(spec, fcT, mT, twH, N, P, mode, s);
+    } else if constexpr (L == 128) {
+        return pass_b_hc<H, 8>(spec, fcT, mT, twH, N, P, mode, s);
+    } else {
+        return pass_b_hc<H, 4>(spec, fcT, mT, twH, N, P, mode, s);
+    }
+}
+
+int pass_b(int H, cf* spec, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode, hipStream_t s) {
+    switch (H) {
+        case 16: return pass_b_h<16>(spec, fcT, mT, twH, N, P, mode, s);
+        case 32: return pass_b_h<32>(spec, fcT, mT, twH, N, P, mode, s);
+        case 64: return pass_b_h<64>(spec, fcT, mT, twH, N, P, mode, s);
+        case 128: return pass_b_h<128>(spec, fcT, mT, twH, N, P, mode, s);
+        case 256: return pass_b_h<256>(spec, fcT, mT, twH, N, P, mode, s);
+        case 512: return pass_b_h<512>(spec, fcT, mT, twH, N, P, mode, s);
+        case 1024: return pass_b_h<1024>(spec, fcT, mT, twH, N, P, mode, s);
+        case 2048: return pass_b_h<2048>(spec, fcT, mT, twH, N, P, mode, s);
+        case 4096: return pass_b_h<4096>(spec, fcT, mT, twH, N, P, mode, s);
+        default: return fail(ADMM_TV_EUNSUPPORTED, "unsupported H");
+    }
+}
+
+int validate(const admm_tv_desc* d) {
+    if (!d) return fail(ADMM_TV_EINVAL, "null descriptor");
+    if (d->B <= 0 || d->C <= 0 || d->H <= 0 || d->W <= 0 || d->maxit < 0 || d->kh < 0 || d->kw < 0)
+        return fail(ADMM_TV_EINVAL, "invalid sizes or maxit");
+    if (d->kh != d->kw) return fail(ADMM_TV_ENONSQUARE, "non-square PSF (the reference's H_t swaps H/W pads)");
+    if (!supported_hw(d->H, d->W))
+        return fail(ADMM_TV_EUNSUPPORTED, "H must be a power of two in [16,4096] and W a power of two in [16,2048]");
+    if (d->kh > d->H || d->kw > d->W) return fail(ADMM_TV_EKERNEL, "PSF larger than the image");
+    return 0;
+}
+
+// setup: twiddle tables, PSF spectrum, Wiener factor (if rho given), centred-PSF multiplier
+int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, const float* rho, hipStream_t s) {
+    ProfScope ps(3, s);
+    const int H = (int)d.H, W = (int)d.W, N = W / 2, k = d.kh;
+    const int nt = 256;
+    hipLaunchKernelGGL(k_tables, dim3((std::max(H, W) + nt - 1) / nt), dim3(nt), 0, s, at<cf>(ws, Lo.twW),
+                       at<cf>(ws, Lo.twH), at<double2>(ws, Lo.twHd), H, W);
+    if (int e = launch_check("k_tables")) return e;
+    if (k > 0) {
+        const int n = k * (N + 1);
+        hipLaunchKernelGGL(k_psf_rows, dim3((n + nt - 1) / nt), dim3(nt), 0, s, kern, at<double2>(ws, Lo.G), k, N, W);
+        if (int e = launch_check("k_psf_rows")) return e;
+    }
+    const int n = (N + 1) * H;
+    if (rho) {
+        hipLaunchKernelGGL(k_spectra, dim3((n + nt - 1) / nt), dim3(nt), 0, s, at<double2>(ws, Lo.G),
+                           at<double2>(ws, Lo.twHd), rho, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), k, H, N, W);
+        if (int e = launch_check("k_spectra")) return e;
+    }
+    return 0;
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int admm_tv_abi_version(void) { return ADMM_TV_ABI_VERSION; }
+
+int admm_tv_supported(int64_t H, int64_t W) { return supported_hw(H, W) ? 1 : 0; }
+
+const char* admm_tv_last_error(void) { return g_err.c_str(); }
+
+int admm_tv_workspace_size(const admm_tv_desc* d, size_t* bytes) {
+    if (int e = validate(d)) return e;
+    if (!bytes) return fail(ADMM_TV_EINVAL, "null bytes");
+    *bytes = make_layout(*d).total;
+    return 0;
+}
+
+int admm_tv_forward(const admm_tv_desc* dp, const float* xin, const float* kern, const float* lam, const float* rho,
+                    float* out, void* ws, size_t ws_bytes, void* stream) {
+    if (int e = validate(dp)) return e;
+    const admm_tv_desc d = *dp;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!xin || !out || !lam || !rho || (d.kh > 0 && !kern)) return fail(ADMM_TV_EINVAL, "null pointer argument");
+    const Layout Lo = make_layout(d);
+    if (!ws || ws_bytes < Lo.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
+        return fail(ADMM_TV_EWORKSPACE, "workspace too small or not 256-byte aligned");
+    const long long P = d.B * d.C;
+    const int H = (int)d.H, W = (int)d.W, N = W / 2;
+    const size_t img_bytes = (size_t)P * H * W * sizeof(float);
+    if (d.maxit == 0) {
+        HIPCHK(hipMemsetAsync(out, 0, img_bytes, s));  // the reference returns x = zeros (deconv.py:61,117)
+        return 0;
+    }
+    if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
+    cf* twW = at<cf>(ws, Lo.twW);
+    cf* twH = at<cf>(ws, Lo.twH);
+    float* fcT = at<float>(ws, Lo.fcT);
+    cf* mT = at<cf>(ws, Lo.mT);
+    cf* spec[2] = {at<cf>(ws, Lo.spec[0]), at<cf>(ws, Lo.spec[1])};
+    float* u[4] = {at<float>(ws, Lo.u[0]), at<float>(ws, Lo.u[1]), at<float>(ws, Lo.u[2]), at<float>(ws, Lo.u[3])};
+    const long long rows = P * H;
+
+    // b = H_t(xin) once (the reference recomputes it every iteration, deconv.py:104)
+    const float* bimg = xin;
+    if (d.kh > 0) {
+        ProfScope ps(3, s);
+        float* bb = at<float>(ws, Lo.b);
+        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(xin, spec[0], twW, rows, s); });
+        if (e) return e;
+        if ((e = pass_b(H, spec[0], fcT, mT, twH, N, (int)P, 1, s))) return e;
+        e = with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec[0], bb, twW, rows, s); });
+        if (e) return e;
+        bimg = bb;
+    }
+    {
+        ProfScope ps(3, s);
+        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, spec[0], twW, rows, s); });
+        if (e) return e;
+    }
+
+    int R = env_int("ADMM_PASSA_R", 0);
+    if (R <= 0) {
+        // rows per strip: as tall as possible while keeping >= ~3 waves per SIMD of strips in flight
+        const int L = std::min(64, N / (N >= 1024 ? 16 : N >= 64 ? 8 : N >= 16 ? 4 : 2));
+        const long long want = 3LL * 1024 * 64 / L;  // strips for ~3 waves/SIMD over 256 CUs
+        R = 16;
+        while (R > 2 && rows / R < want) R /= 2;
+    }
+    if (R > H) R = H;
+
+    int cur = 0, uin = 0;  // spec[cur] holds the current r spectra; u[2*uin], u[2*uin+1] = u_x, u_y in
+    for (int it = 1; it <= d.maxit; ++it) {
+        {
+            ProfScope ps(1, s);
+            if (int e = pass_b(H, spec[cur], fcT, mT, twH, N, (int)P, 0, s)) return e;
+        }
+        if (it == d.maxit) {
+            ProfScope ps(3, s);
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec[cur], out, twW, rows, s); });
+            if (e) return e;
+            break;
+        }
+        const bool first = (it == 1);
+        float* uxi = u[2 * uin];
+        float* uyi = u[2 * uin + 1];
+        float* uxo = u[2 * (1 - uin)];
+        float* uyo = u[2 * (1 - uin) + 1];
+        const float* nsq = nullptr;
+        if (d.iso) {
+            ProfScope ps(2, s);
+            IsoArgs ia{spec[cur], uxi, uyi, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
+                       (long long)Lo.ngroups * H};
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::iso_norm(ia, first, s); });
+            if (e) return e;
+            const long long n4 = 2LL * H * W / 4;
+            hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                               at<float4>(ws, Lo.part), at<float4>(ws, Lo.nsq), Lo.ngroups, n4);
+            if ((e = launch_check("k_iso_reduce"))) return e;
+            nsq = at<float>(ws, Lo.nsq);
+        }
+        {
+            ProfScope ps(0, s);
+            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, lam, rho, twW, H, R, rows / R};
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, s); });
+            if (e) return e;
+        }
+        cur = 1 - cur;
+        uin = 1 - uin;
+    }
+    return 0;
+}
+
+int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float* kern, float* out, void* ws,
+                          size_t ws_bytes, void* stream) {
+    if (int e = validate(dp)) return e;
+    const admm_tv_desc d = *dp;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const Layout Lo = make_layout(d);
+    if (!ws || ws_bytes < Lo.total) return fail(ADMM_TV_EWORKSPACE, "workspace too small");
+    const long long P = d.B * d.C;
+    const int H = (int)d.H, W = (int)d.W, N = W / 2;
+    if (d.kh == 0) {
+        HIPCHK(hipMemcpyAsync(out, xin, (size_t)P * H * W * sizeof(float), hipMemcpyDeviceToDevice, s));
+        return 0;
+    }
+    if (int e = setup(d, Lo, ws, kern, nullptr, s)) return e;
+    const int n = (N + 1) * H;
+    // k_spectra needs a rho pointer: point it at a zeroed float inside the workspace (fcT region)
+    HIPCHK(hipMemsetAsync(at<float>(ws, Lo.fcT), 0, sizeof(float), s));
+    hipLaunchKernelGGL(k_spectra, dim3((n + 255) / 256), dim3(256), 0, s, at<double2>(ws, Lo.G),
+                       at<double2>(ws, Lo.twHd), at<float>(ws, Lo.fcT), at<float>(ws, Lo.spec[1]),
+                       at<cf>(ws, Lo.mT), d.kh, H, N, W);
+    if (int e = launch_check("k_spectra")) return e;
+    cf* twW = at<cf>(ws, Lo.twW);
+    const long long rows = P * H;
+    int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(xin, at<cf>(ws, Lo.spec[0]), twW, rows, s); });
+    if (e) return e;
+    if ((e = pass_b(H, at<cf>(ws, Lo.spec[0]), nullptr, at<cf>(ws, Lo.mT), at<cf>(ws, Lo.twH), N, (int)P, 1, s)))
+        return e;
+    return with_row(N, [&](auto ops) { return decltype(ops)::c2r(at<cf>(ws, Lo.spec[0]), out, twW, rows, s); });
+}
+
+int admm_tv_profile_enable(int enable) {
+    g_prof.on = enable != 0;
+    return 0;
+}
+
+int admm_tv_profile_reset(void) {
+    for (auto& r : g_prof.recs) {
+        (void)hipEventSynchronize(r.b);
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.recs.clear();
+    for (int i = 0; i < 4; ++i) {
+        g_prof.ms[i] = 0;
+        g_prof.n[i] = 0;
+    }
+    return 0;
+}
+
+int admm_tv_profile_read(double* ms4, int64_t* count4) {
+    for (auto& r : g_prof.recs) {
+        if (hipEventSynchronize(r.b) != hipSuccess) return fail(ADMM_TV_EHIP, "hipEventSynchronize");
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_prof.ms[r.kind] += ms;
+            g_prof.n[r.kind] += 1;
+        }
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.recs.clear();
+    for (int i = 0; i < 4; ++i) {
+        if (ms4) ms4[i] = g_prof.ms[i];
+        if (count4) count4[i] = g_prof.n[i];
+    }
+    return 0;
+}
+
+}  // extern "C"

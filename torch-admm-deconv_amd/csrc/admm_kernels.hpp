@@ -1,0 +1,535 @@
+// admm_kernels.hpp -- HIP kernels of the MI355X ADMM-TV solver (gfx950).
+//
+// Data layout in HBM (P = B*C planes, N = W/2):
+//   images  float [P][H][W]      (xin, b, u_x, u_y, out)
+//   spectra cf    [P][H][N]      packed real row spectra: element 0 holds
+//                                (X[0], X[N]) (DC and Nyquist are real), 1..N-1 hold X[k].
+//                                Exactly H*W floats per plane, rows 8N-byte aligned.
+//   fcT     float [N+1][H]       Wiener factor / (2HW), transposed (column-major in ky)
+//   mT      cf    [N+1][H]       centred-PSF spectrum / (2HW), transposed
+//
+// One ADMM iteration (deconv.py:103-115) is
+//   pass B  (column pass, in place): spec = colIFFT( fc * colFFT(spec) )   -> x row spectra
+//   pass A  (row pass): x = rowIFFT(spec) (+1 halo row each side), Dx, Dy, shrink,
+//           dual update of u (ping-pong), v = Dx^T w_x + Dy^T w_y with w = z - u,
+//           r = b + rho v, spec' = rowFFT(r)
+// The row transform scaling is folded into fcT / mT.
+#pragma once
+#include "fft_core.hpp"
+
+namespace admm {
+
+// ---------------------------------------------------------------------------
+// packed real-row transforms for one sub-group of L lanes (natural layout)
+// ---------------------------------------------------------------------------
+template <int N> struct RowXf {
+    static constexpr int E = RowCfg<N>::E;
+    static constexpr int L = N / E;
+    static constexpr int W = 2 * N;
+    static_assert(L <= 64, "row transforms keep one row inside one wave");
+
+    // p[j] = v at index N - (t + L j)  (j = 0 at t = 0 is the DC slot; unused)
+    __device__ __forceinline__ static void partner(const cf (&v)[E], cf (&p)[E], int t) {
+        const int src = (L - t) & (L - 1);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            float a = __shfl(v[E - 1 - j].x, src, L);
+            float b = __shfl(v[E - 1 - j].y, src, L);
+            p[j] = (t == 0) ? v[(E - j) & (E - 1)] : mkc(a, b);
+        }
+    }
+
+    // packed spectrum (== 2*rfft of a real row y) -> pixel pairs (2W * y).
+    // tw: exp(-2 pi i k / W), k in [0, W)  (LDS)
+    __device__ __forceinline__ static void c2r(cf (&v)[E], const RowBuf& buf, const cf* __restrict__ tw, int t) {
+        cf p[E];
+        partner(v, p, t);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const int k = t + L * j;
+            cf z;
+            if (j == 0 && t == 0) {
+                z = mkc(v[0].x + v[0].y, v[0].x - v[0].y);
+            } else {
+                cf pc = cconj(p[j]);
+                cf e = cadd(v[j], pc);
+                cf o = cmulc(csub(v[j], pc), tw[k]);  // * exp(+2 pi i k/W)
+                z = mkc(e.x - o.y, e.y + o.x);         // e + i o
+            }
+            v[j] = z;
+        }
+        fft<N, L, +1, 0, 2>(v, buf, tw, t);
+    }
+
+    // pixel pairs of a real row r -> packed spectrum 2*rfft(r)
+    __device__ __forceinline__ static void r2c(cf (&v)[E], const RowBuf& buf, const cf* __restrict__ tw, int t) {
+        fft<N, L, -1, 0, 2>(v, buf, tw, t);
+        cf p[E];
+        partner(v, p, t);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const int k = t + L * j;
+            cf z;
+            if (j == 0 && t == 0) {
+                z = mkc(2.f * (v[0].x + v[0].y), 2.f * (v[0].x - v[0].y));
+            } else {
+                cf pc = cconj(p[j]);
+                cf s = cadd(v[j], pc);
+                cf d = cmul(csub(v[j], pc), tw[k]);  // w^k (Z - conj Z~)
+                z = mkc(s.x + d.y, s.y - d.x);        // s - i d
+            }
+            v[j] = z;
+        }
+    }
+};
+
+// soft shrink  sign(a) max(|a| - tau, 0)   (deconv.py:15-16); NaN propagates
+__device__ __forceinline__ float soft(float a, float tau) {
+    float m = fabsf(a) - tau;
+    m = (m < 0.f) ? 0.f : m;
+    return copysignf(m, a);
+}
+// block-shrink factor max(1 - tau/(sqrt(s + 1e-15) + 1e-15), 0)   (deconv.py:19-24)
+__device__ __forceinline__ float block_factor(float sumsq, float tau) {
+    float n = sqrtf(sumsq + 1e-15f);
+    float f = 1.f - tau / (n + 1e-15f);
+    return f < 0.f ? 0.f : f;
+}
+
+// ---------------------------------------------------------------------------
+// setup kernels
+// ---------------------------------------------------------------------------
+// twiddle tables: twW[k] = exp(-2 pi i k/W) (k < W), twH[k] = exp(-2 pi i k/H) (k < H),
+// twHd in fp64 for the PSF spectrum.
+__global__ void k_tables(cf* __restrict__ twW, cf* __restrict__ twH, double2* __restrict__ twHd, int H, int W) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < W) {
+        double s, c;
+        sincospi(2.0 * i / W, &s, &c);
+        twW[i] = mkc((float)c, (float)-s);
+    }
+    if (i < H) {
+        double s, c;
+        sincospi(2.0 * i / H, &s, &c);
+        twH[i] = mkc((float)c, (float)-s);
+        twHd[i] = make_double2(c, -s);
+    }
+}
+
+// G[a][kx] = sum_b kern[a][b] exp(-2 pi i b kx / W), kx in [0, N], in fp64
+__global__ void k_psf_rows(const float* __restrict__ kern, double2* __restrict__ G, int k, int N, int W) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k * (N + 1)) return;
+    const int a = i / (N + 1), kx = i % (N + 1);
+    double re = 0.0, im = 0.0;
+    for (int b = 0; b < k; ++b) {
+        const long long m = ((long long)b * kx) % W;
+        double s, c;
+        sincospi(2.0 * (double)m / W, &s, &c);
+        const double w = (double)kern[a * k + b];
+        re += w * c;
+        im -= w * s;
+    }
+    G[i] = make_double2(re, im);
+}
+
+// fcT[kx][ky] = 1 / (|sigma|^2 + rho (|Dx^|^2 + |Dy^|^2)) / (2HW);
+// mT[kx][ky] = sigma * exp(+2 pi i c (ky/H + kx/W)) / (2HW)  (centred PSF, c = k/2)
+__global__ void k_spectra(const double2* __restrict__ G, const double2* __restrict__ twHd,
+                          const float* __restrict__ rho_p, float* __restrict__ fcT, cf* __restrict__ mT, int k,
+                          int H, int N, int W) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (N + 1) * H) return;
+    const int kx = i / H, ky = i % H;
+    double sr = 1.0, si = 0.0;
+    if (k > 0) {
+        sr = 0.0;
+        for (int a = 0; a < k; ++a) {
+            const double2 w = twHd[((long long)a * ky) % H];
+            const double2 g = G[a * (N + 1) + kx];
+            sr += w.x * g.x - w.y * g.y;
+            si += w.x * g.y + w.y * g.x;
+        }
+    }
+    const double rho = (double)rho_p[0];
+    const double sx = sinpi((double)kx / W), sy = sinpi((double)ky / H);
+    const double lap = 4.0 * sx * sx + 4.0 * sy * sy;
+    const double scale = 1.0 / (2.0 * (double)H * (double)W);
+    fcT[i] = (float)(scale / (sr * sr + si * si + rho * lap));
+    if (k > 0) {
+        const int c = k / 2;  // ceil((k-1)/2): anchor of the reference's H_t
+        const long long ph = (long long)c * ky * W + (long long)c * kx * H;  // units of 1/(H W)
+        const long long HW = (long long)H * W;
+        double s, co;
+        sincospi(2.0 * (double)(ph % HW) / (double)HW, &s, &co);
+        mT[i] = mkc((float)((sr * co - si * s) * scale), (float)((sr * s + si * co) * scale));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// row transforms of whole images (one sub-group of L lanes per row)
+// ---------------------------------------------------------------------------
+template <int N> struct RowKernelGeom {
+    static constexpr int E = RowCfg<N>::E, L = N / E, W = 2 * N;
+    static constexpr int NT = 256, SG = NT / L;
+    static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * RowBuf::slots(N)); }
+};
+
+__device__ __forceinline__ void load_tw(cf* dst, const cf* __restrict__ src, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+// real rows -> packed row spectra
+template <int N>
+__global__ void __launch_bounds__(256) k_row_r2c(const float* __restrict__ img, cf* __restrict__ spec,
+                                                 const cf* __restrict__ twW_g, long long rows) {
+    using G = RowKernelGeom<N>;
+    constexpr int E = G::E, L = G::L;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, twW_g, G::W);
+    __syncthreads();
+    const int sgl = threadIdx.x / L, t = threadIdx.x % L;
+    const long long row = (long long)blockIdx.x * G::SG + sgl;
+    if (row >= rows) return;
+    RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
+    const cf* src = reinterpret_cast<const cf*>(img + row * G::W);
+    cf v[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = src[t + L * j];
+    RowXf<N>::r2c(v, buf, tw, t);
+    cf* dst = spec + row * N;
+#pragma unroll
+    for (int j = 0; j < E; ++j) dst[t + L * j] = v[j];
+}
+
+// packed row spectra -> real rows
+template <int N>
+__global__ void __launch_bounds__(256) k_row_c2r(const cf* __restrict__ spec, float* __restrict__ img,
+                                                 const cf* __restrict__ twW_g, long long rows) {
+    using G = RowKernelGeom<N>;
+    constexpr int E = G::E, L = G::L;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, twW_g, G::W);
+    __syncthreads();
+    const int sgl = threadIdx.x / L, t = threadIdx.x % L;
+    const long long row = (long long)blockIdx.x * G::SG + sgl;
+    if (row >= rows) return;
+    RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
+    const cf* src = spec + row * N;
+    cf v[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = src[t + L * j];
+    RowXf<N>::c2r(v, buf, tw, t);
+    cf* dst = reinterpret_cast<cf*>(img + row * G::W);
+#pragma unroll
+    for (int j = 0; j < E; ++j) dst[t + L * j] = v[j];
+}
+
+// ---------------------------------------------------------------------------
+// pass B: column FFT -> multiply -> column IFFT, in place, C columns per block
+// MODE 0: real Wiener factor fcT;  MODE 1: complex multiplier mT (PSF transpose)
+// ---------------------------------------------------------------------------
+template <int H, int C> struct ColGeom {
+    static constexpr int E = RowCfg<H>::E, L = H / E, NT = C * L;
+    static constexpr int SYNC = 1;
+    static constexpr size_t lds_bytes() { return sizeof(cf) * (H + (size_t)H * C); }
+};
+
+template <int H, int C, int MODE>
+__global__ void __launch_bounds__(C * (H / RowCfg<H>::E)) k_pass_b(cf* __restrict__ spec, const float* __restrict__ fcT,
+                                                              const cf* __restrict__ mT, const cf* __restrict__ twH_g,
+                                                              int N, int colblocks) {
+    using G = ColGeom<H, C>;
+    constexpr int E = G::E, L = G::L;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* data = tw + H;
+    load_tw(tw, twH_g, H);
+    const int tid = threadIdx.x;
+    const int c = tid % C, t = tid / C;
+    const int p = blockIdx.x / colblocks, cb = blockIdx.x % colblocks;
+    const int col = cb * C + c;
+    cf* base = spec + (size_t)p * H * N + col;
+    cf v[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = base[(size_t)(t + L * j) * N];
+    __syncthreads();
+    ColBuf<C> buf{data + c};
+    fft<H, L, -1, 1, 1>(v, buf, tw, t);
+    if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H-ky]
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < E; ++j) buf.at(t + L * j) = v[j];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const int ky = t + L * j;
+        if (col == 0) {
+            const cf q = cconj(buf.at((H - ky) & (H - 1)));
+            if constexpr (MODE == 0) {
+                const float f0 = fcT[ky], fn = fcT[(size_t)N * H + ky];
+                const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
+                v[j] = mkc(a * v[j].x + b * q.x, a * v[j].y + b * q.y);
+            } else {
+                const cf m0 = mT[ky], mn = mT[(size_t)N * H + ky];
+                const cf a = mkc(0.5f * (m0.x + mn.x), 0.5f * (m0.y + mn.y));
+                const cf b = mkc(0.5f * (m0.x - mn.x), 0.5f * (m0.y - mn.y));
+                v[j] = cadd(cmul(v[j], a), cmul(q, b));
+            }
+        } else {
+            if constexpr (MODE == 0) {
+                v[j] = cscale(v[j], fcT[(size_t)col * H + ky]);
+            } else {
+                v[j] = cmul(v[j], mT[(size_t)col * H + ky]);
+            }
+        }
+    }
+    fft<H, L, +1, 1, 1>(v, buf, tw, t);
+#pragma unroll
+    for (int j = 0; j < E; ++j) base[(size_t)(t + L * j) * N] = v[j];
+}
+
+// ---------------------------------------------------------------------------
+// pass A: the fused row pass of one ADMM iteration, one sub-group per strip of R rows
+// ---------------------------------------------------------------------------
+struct PassAArgs {
+    const cf* sin;      // x row spectra (output of pass B)     [P][H][N]
+    cf* sout;           // r row spectra for the next pass B     [P][H][N]
+    const float* b;     // H_t(xin)                              [P][H][W]
+    const float* uxi;   // u_x, u_y of the previous iteration    [P][H][W]
+    const float* uyi;
+    float* uxo;         // u_x, u_y of this iteration (ping-pong)
+    float* uyo;
+    const float* nsq;   // iso: per-pixel sum over (B,C) of a_x^2, a_y^2  [2][H][W]
+    const float* lam;
+    const float* rho;
+    const cf* twW;      // [W]
+    int H;
+    int R;              // rows per strip (divides H)
+    long long nstrips;
+};
+
+template <int N, bool ISO, bool FIRST>
+__global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
+    using G = RowKernelGeom<N>;
+    constexpr int E = G::E, L = G::L, W = G::W;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, a.twW, W);
+    __syncthreads();
+    const int sgl = threadIdx.x / L, t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * G::SG + sgl;
+    if (strip >= a.nstrips) return;
+    const int H = a.H, R = a.R;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    const float rho = a.rho[0];
+    const float tau = a.lam[0] / rho;
+
+    const cf* sp = a.sin + (size_t)p * H * N;
+    cf* so = a.sout + (size_t)p * H * N;
+    const size_t poff = (size_t)p * H * W;
+    const cf* bimg = reinterpret_cast<const cf*>(a.b + poff);
+    const cf* uxi = reinterpret_cast<const cf*>(a.uxi + poff);
+    const cf* uyi = reinterpret_cast<const cf*>(a.uyi + poff);
+    cf* uxo = reinterpret_cast<cf*>(a.uxo + poff);
+    cf* uyo = reinterpret_cast<cf*>(a.uyo + poff);
+    const cf* nsx = reinterpret_cast<const cf*>(a.nsq);
+    const cf* nsy = reinterpret_cast<const cf*>(a.nsq + (size_t)H * W);
+
+    cf xprev[E], xcur[E], wxp[E], wyp[E];
+    {
+        const int g = (i0 - 1 + H) & (H - 1);
+#pragma unroll
+        for (int j = 0; j < E; ++j) xprev[j] = sp[(size_t)g * N + t + L * j];
+        RowXf<N>::c2r(xprev, buf, tw, t);
+    }
+    for (int rr = 0; rr <= R; ++rr) {
+        const int g = (i0 + rr) & (H - 1);
+        const size_t ro = (size_t)g * N;  // row offset in cf units (spectrum and pixel pairs alike)
+#pragma unroll
+        for (int j = 0; j < E; ++j) xcur[j] = sp[ro + t + L * j];
+        RowXf<N>::c2r(xcur, buf, tw, t);
+
+        // ---- y direction: dy = x[g] - x[g-1]; z_y, u_y, w_y of row g
+        cf wyc[E];
+        {
+            cf uy[E], fy[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                uy[j] = FIRST ? mkc(0.f, 0.f) : uyi[ro + t + L * j];
+                if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
+            }
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const float a0 = (xcur[j].x - xprev[j].x) + uy[j].x;
+                const float a1 = (xcur[j].y - xprev[j].y) + uy[j].y;
+                float z0, z1;
+                if constexpr (ISO) {
+                    z0 = block_factor(fy[j].x, tau) * a0;
+                    z1 = block_factor(fy[j].y, tau) * a1;
+                } else {
+                    z0 = soft(a0, tau);
+                    z1 = soft(a1, tau);
+                }
+                const float n0 = a0 - z0, n1 = a1 - z1;  // u_y(new)
+                uy[j] = mkc(n0, n1);
+                wyc[j] = mkc(z0 - n0, z1 - n1);
+            }
+            if (rr < R) {
+#pragma unroll
+                for (int j = 0; j < E; ++j) uyo[ro + t + L * j] = uy[j];
+            }
+        }
+
+        // ---- finalize row g-1: v = Dx^T w_x + Dy^T w_y, r = b + rho v, row FFT
+        if (rr >= 1) {
+            const int gm = (g - 1 + H) & (H - 1);
+            const size_t rm = (size_t)gm * N;
+            cf r[E], sh[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) sh[j].x = __shfl(wxp[j].x, (t + 1) & (L - 1), L);
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const float wr = (t == L - 1) ? sh[(j + 1) & (E - 1)].x : sh[j].x;  // w_x at pixel q1+1
+                const cf bb = bimg[rm + t + L * j];
+                const float v0 = (wxp[j].x - wxp[j].y) + (wyp[j].x - wyc[j].x);
+                const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
+                r[j] = mkc(bb.x + rho * v0, bb.y + rho * v1);
+            }
+            RowXf<N>::r2c(r, buf, tw, t);
+#pragma unroll
+            for (int j = 0; j < E; ++j) so[rm + t + L * j] = r[j];
+        }
+
+        // ---- x direction: dx = x[g][j] - x[g][j-1]; z_x, u_x, w_x of row g
+        if (rr < R) {
+            cf ux[E], fx[E], sh[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                ux[j] = FIRST ? mkc(0.f, 0.f) : uxi[ro + t + L * j];
+                if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
+                sh[j].x = __shfl(xcur[j].y, (t - 1) & (L - 1), L);
+            }
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const float xl = (t == 0) ? sh[(j - 1) & (E - 1)].x : sh[j].x;  // x at pixel q0-1
+                const float a0 = (xcur[j].x - xl) + ux[j].x;
+                const float a1 = (xcur[j].y - xcur[j].x) + ux[j].y;
+                float z0, z1;
+                if constexpr (ISO) {
+                    z0 = block_factor(fx[j].x, tau) * a0;
+                    z1 = block_factor(fx[j].y, tau) * a1;
+                } else {
+                    z0 = soft(a0, tau);
+                    z1 = soft(a1, tau);
+                }
+                const float n0 = a0 - z0, n1 = a1 - z1;
+                ux[j] = mkc(n0, n1);
+                wxp[j] = mkc(z0 - n0, z1 - n1);
+            }
+#pragma unroll
+            for (int j = 0; j < E; ++j) uxo[ro + t + L * j] = ux[j];
+        }
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            wyp[j] = wyc[j];
+            xprev[j] = xcur[j];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// iso pass A1: per-pixel partial sums over a group of planes of a_x^2, a_y^2
+// (a = D x + u), one sub-group per (plane group, row)
+// ---------------------------------------------------------------------------
+struct IsoArgs {
+    const cf* sin;
+    const float* uxi;
+    const float* uyi;
+    float* partial;  // [ngroups][2][H][W]
+    const cf* twW;
+    int P, H, ppg;   // planes per group
+    long long nitems;  // ngroups * H
+};
+
+template <int N, bool FIRST>
+__global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
+    using G = RowKernelGeom<N>;
+    constexpr int E = G::E, L = G::L, W = G::W;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, a.twW, W);
+    __syncthreads();
+    const int sgl = threadIdx.x / L, t = threadIdx.x % L;
+    const long long item = (long long)blockIdx.x * G::SG + sgl;
+    if (item >= a.nitems) return;
+    const int H = a.H;
+    const int g = (int)(item % H);
+    const int grp = (int)(item / H);
+    const int gm = (g - 1 + H) & (H - 1);
+    RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    cf sx[E], sy[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) sx[j] = sy[j] = mkc(0.f, 0.f);
+    const int p1 = min(a.P, (grp + 1) * a.ppg);
+    for (int p = grp * a.ppg; p < p1; ++p) {
+        const cf* sp = a.sin + (size_t)p * H * N;
+        cf xp[E], xc[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            xp[j] = sp[(size_t)gm * N + t + L * j];
+            xc[j] = sp[(size_t)g * N + t + L * j];
+        }
+        RowXf<N>::c2r(xp, buf, tw, t);
+        RowXf<N>::c2r(xc, buf, tw, t);
+        const size_t ro = (size_t)p * H * N + (size_t)g * N;  // cf units == pixel pairs
+        const cf* uxi = reinterpret_cast<const cf*>(a.uxi);
+        const cf* uyi = reinterpret_cast<const cf*>(a.uyi);
+        cf sh[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) sh[j].x = __shfl(xc[j].y, (t - 1) & (L - 1), L);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const cf ux = FIRST ? mkc(0.f, 0.f) : uxi[ro + t + L * j];
+            const cf uy = FIRST ? mkc(0.f, 0.f) : uyi[ro + t + L * j];
+            const float xl = (t == 0) ? sh[(j - 1) & (E - 1)].x : sh[j].x;
+            const float ax0 = (xc[j].x - xl) + ux.x, ax1 = (xc[j].y - xc[j].x) + ux.y;
+            const float ay0 = (xc[j].x - xp[j].x) + uy.x, ay1 = (xc[j].y - xp[j].y) + uy.y;
+            sx[j].x += ax0 * ax0;
+            sx[j].y += ax1 * ax1;
+            sy[j].x += ay0 * ay0;
+            sy[j].y += ay1 * ay1;
+        }
+    }
+    cf* px = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 0) * H * W) + (size_t)g * N;
+    cf* py = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 1) * H * W) + (size_t)g * N;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        px[t + L * j] = sx[j];
+        py[t + L * j] = sy[j];
+    }
+}
+
+// nsq[k] = sum_g partial[g][k], k over 2*H*W, fixed order (deterministic)
+__global__ void k_iso_reduce(const float4* __restrict__ partial, float4* __restrict__ nsq, int ngroups,
+                             long long n4) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    float4 s = partial[i];
+    for (int g = 1; g < ngroups; ++g) {
+        const float4 q = partial[(size_t)g * n4 + i];
+        s.x += q.x;
+        s.y += q.y;
+        s.z += q.z;
+        s.w += q.w;
+    }
+    nsq[i] = s;
+}
+
+}  // namespace admm
