@@ -110,7 +110,7 @@ def main():
     B, C, H, W, kind, k, maxit, iso, desc = cfg
 
     from admmtor import _native
-    from admmtor.eops.deconv import fft_admm_tv
+    from admmtor.sharded import sharded_fft_admm_tv
     from admmtor.synth import CONFIG_SEED, blurred_batch, make_psf
 
     # rank-local shard of synthetic blurred images, generated directly in HBM
@@ -121,11 +121,8 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        if world > 1:
-            for t in (psf, lam, rho):
-                if t.numel():
-                    dist.broadcast(t, src=0)
-        return fft_admm_tv(x, lam, rho, psf, iso, maxit)
+        # RCCL broadcast of PSF / lambda / rho from rank 0 (no-op at N=1), then the local shard
+        return sharded_fft_admm_tv(x, lam, rho, psf, iso, maxit)
 
     for _ in range(args.warmup):
         out = step()

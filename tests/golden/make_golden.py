@@ -186,6 +186,32 @@ def main():
     grab("kernel_2d", lambda: ref.fft_admm_tv(x4, 0.01, 0.02, torch.rand(3, 3), False, 2))
     grab("maxit_0_ok", lambda: ref.fft_admm_tv(x4, 0.01, 0.02, torch.empty(0), False, 0))
     meta["errors"] = errs
+
+    # ---- ADMMDeconv construction: seeded init values + state_dict layout ---------------
+    import subprocess
+    code = r"""
+import json, torch
+from admmtor.elayers.admmdeconv import ADMMDeconv
+cases = [dict(kern_size=(3, 3), max_iters=10), dict(kern_size=(), max_iters=100, iso=True),
+         dict(kern_size=(5, 5), max_iters=7, lmbda=0.02, rho=0.04, iso=False, bias=True),
+         dict(kern_size=(), max_iters=3, lmbda=0.0, rho=0.5)]
+out = []
+for i, c in enumerate(cases):
+    torch.manual_seed(100 + i)
+    m = ADMMDeconv(**c)
+    sd = m.state_dict()
+    out.append({"kwargs": {k: (list(v) if isinstance(v, tuple) else v) for k, v in c.items()},
+                "keys": list(sd.keys()),
+                "params": [n for n, _ in m.named_parameters()],
+                "buffers": [n for n, _ in m.named_buffers()],
+                "values": {k: v.flatten().tolist() for k, v in sd.items()},
+                "shapes": {k: list(v.shape) for k, v in sd.items()}})
+print(json.dumps(out))
+"""
+    env = dict(os.environ, PYTHONPATH="/root/reference/src", PYTHONDONTWRITEBYTECODE="1")
+    res = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True, cwd="/tmp")
+    with open(os.path.join(OUT, "module_init.json"), "w") as f:
+        f.write(res.stdout)
     with open(os.path.join(OUT, "errors.json"), "w") as f:
         json.dump(errs, f, indent=1, sort_keys=True)
     with open(os.path.join(OUT, "meta.json"), "w") as f:

@@ -1,0 +1,82 @@
+"""The C-ABI library builds for gfx950, loads, and exports every symbol include/admm_tv.h declares.
+
+Host-only entry points (version, size checks, workspace sizing, error codes) are
+exercised; nothing here launches a kernel (no GPU in the build container).
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "admm_tv.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(admm_tv_\w+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree():
+    from admmtor import _native
+    assert declared_functions() == sorted(_native.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    from admmtor import _native
+    so = _native.lib_path()
+    assert os.path.exists(so), "build the library first (python __graft_entry__.py build)"
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\sT\s(admm_tv_\w+)", out))
+    missing = set(declared_functions()) - exported
+    assert not missing, missing
+    lib = _native.load()
+    for name in declared_functions():
+        assert getattr(lib, name) is not None
+
+
+def test_library_is_gfx950_code():
+    from admmtor import _native
+    blob = open(_native.lib_path(), "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the embedded code object targets gfx950 only
+    assert b"gfx942" not in blob and b"sm_" not in blob[:0]  # no other GPU target bundled
+
+
+def test_host_entry_points():
+    from admmtor import _native
+    lib = _native.load()
+    assert lib.admm_tv_abi_version() == 1
+    assert _native.supported(1024, 1024) and _native.supported(16, 2048) and _native.supported(4096, 16)
+    assert not _native.supported(15, 17) and not _native.supported(1024, 4096) and not _native.supported(8, 64)
+    d = _native.desc(64, 3, 1024, 1024, 21, False, 50)
+    ws = _native.workspace_size(d)
+    img = 64 * 3 * 1024 * 1024 * 4
+    assert 7 * img <= ws <= 7 * img + (64 << 20)  # 2 spectra + 4 u + b (+ small tables)
+    d_iso = _native.desc(16, 3, 512, 512, 0, True, 100)
+    assert _native.workspace_size(d_iso) > 6 * 16 * 3 * 512 * 512 * 4
+
+
+@pytest.mark.parametrize("field,value,code", [
+    ("kw", 5, -3),      # non-square PSF -> ADMM_TV_ENONSQUARE
+    ("H", 24, -2),      # unsupported size
+    ("maxit", -1, -1),  # invalid
+    ("kh", 99, -3),
+])
+def test_host_error_codes(field, value, code):
+    from admmtor import _native
+    d = _native.desc(1, 1, 64, 64, 3, False, 5)
+    setattr(d, field, value)
+    n = ctypes.c_size_t(0)
+    assert _native.load().admm_tv_workspace_size(ctypes.byref(d), ctypes.byref(n)) == code
+    assert _native.load().admm_tv_last_error()
+
+
+def test_psf_larger_than_image_is_rejected():
+    from admmtor import _native
+    d = _native.desc(1, 1, 16, 16, 21, False, 5)
+    n = ctypes.c_size_t(0)
+    assert _native.load().admm_tv_workspace_size(ctypes.byref(d), ctypes.byref(n)) == -6

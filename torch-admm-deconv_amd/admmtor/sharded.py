@@ -1,0 +1,94 @@
+"""Batch-sharded ADMM-TV over the GPUs of a node (one process per GPU, RCCL over xGMI).
+
+SURVEY.md §8 e1: with soft shrinkage (iso=False) every (b, c) plane is an
+independent problem, so a batch is split across ranks with NO per-iteration
+communication.  The only collectives are a broadcast of the PSF, lambda and rho
+from rank 0 (a few KB: every rank then builds its own Wiener factor) and,
+optionally, a final gather of the outputs.  iso=True couples the whole batch
+through the per-pixel (B, C) norm and needs a per-iteration all-reduce; that
+mode is not sharded yet (raises for world > 1).
+
+The reference has no distributed code at all; this module is the
+multi-GPU layer of the MI355X build.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+__all__ = ["shard_bounds", "broadcast_params", "sharded_fft_admm_tv"]
+
+
+def shard_bounds(total: int, world: int, rank: int):
+    """Contiguous near-equal split of `total` items: the [start, stop) of `rank`."""
+    base, rem = divmod(total, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def _as_tensor(v, device, dtype=torch.float32):
+    if isinstance(v, torch.Tensor):
+        return v.detach().reshape(-1)[:1].to(device=device, dtype=dtype).clone()
+    return torch.tensor([float(v)], device=device, dtype=dtype)
+
+
+def broadcast_params(kern: torch.Tensor, lmbd, rho, group=None, src: int = 0, device=None):
+    """Broadcast (kern, lambda, rho) from `src` to every rank of `group`.
+
+    Non-source ranks only need to pass a kern of the right size (its values are
+    overwritten).  Returns device tensors: kern (1,1,k,k) or empty, lambda (1,), rho (1,).
+    """
+    device = device or (kern.device if kern.numel() else torch.device("cpu"))
+    k = kern.detach().to(device=device, dtype=torch.float32).contiguous().clone() if kern.numel() else \
+        torch.empty(0, device=device)
+    lam = _as_tensor(lmbd, device)
+    rh = _as_tensor(rho, device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        packed = torch.cat([lam, rh, k.reshape(-1)])  # one collective for all three
+        dist.broadcast(packed, src=src, group=group)
+        lam, rh = packed[0:1], packed[1:2]
+        if k.numel():
+            k = packed[2:].reshape(k.shape)
+    return k, lam, rh
+
+
+def sharded_fft_admm_tv(x_local: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool = False, maxit: int = 100,
+                        *, group=None, gather: Optional[str] = None, total_batch: Optional[int] = None,
+                        solver: Optional[Callable] = None) -> torch.Tensor:
+    """Solve this rank's batch shard; optionally all-gather the full output.
+
+    x_local      (b_r, C, H, W) shard owned by this rank (see shard_bounds)
+    gather       None -> return the local result; "all" -> every rank gets the
+                 full (B, C, H, W) output (all_gather over RCCL, shards padded
+                 to equal size internally)
+    solver       defaults to admmtor.eops.deconv.fft_admm_tv (the HIP path)
+    """
+    if solver is None:
+        from admmtor.eops.deconv import fft_admm_tv as solver
+    world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+    if world > 1 and iso:
+        raise NotImplementedError("iso=True couples the whole batch (per-pixel norm over B and C): "
+                                  "batch sharding needs a per-iteration all-reduce, not implemented yet")
+    k, lam, rh = broadcast_params(kern, lmbd, rho, group=group, device=x_local.device)
+    out = solver(x_local, lam, rh, k, iso, maxit)
+    if gather is None or world == 1:
+        return out
+    if gather != "all":
+        raise ValueError("gather must be None or 'all'")
+    B = total_batch
+    if B is None:
+        n = torch.tensor([x_local.shape[0]], device=x_local.device)
+        dist.all_reduce(n, group=group)
+        B = int(n.item())
+    per = -(-B // world)
+    pad = torch.zeros((per,) + tuple(out.shape[1:]), dtype=out.dtype, device=out.device)
+    pad[: out.shape[0]] = out
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    parts = []
+    for r in range(world):
+        s, e = shard_bounds(B, world, r)
+        parts.append(bufs[r][: e - s])
+    return torch.cat(parts, 0)
