@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-planes", type=int, default=6, help="CPU baseline sample: planes of 1024^2")
-    ap.add_argument("--cpu-iters", type=int, default=12, help="CPU baseline sample: timed iterations")
+    ap.add_argument("--cpu-iters", type=int, default=36, help="CPU baseline sample: timed iterations")
     return ap.parse_args()
 
 

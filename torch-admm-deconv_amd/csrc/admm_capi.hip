@@ -219,7 +219,7 @@ template <int H> int pass_b_h(cf* spec, const float* fcT, const cf* mT, const cf
                               hipStream_t s) {
     constexpr int L = ColGeom<H, 1>::L;
     if constexpr (L <= 64) {
-        int C = env_int("ADMM_PASSB_C", 16);
+        int C = env_int("ADMM_PASSB_C", 8);
         if (C > N) C = N;
         if (C >= 16) return pass_b_hc<H, 16>(spec, fcT, mT, twH, N, P, mode, s);
         return pass_b_hc<H, 8>(spec, fcT, mT, twH, N, P, mode, s);
@@ -341,10 +341,11 @@ int admm_tv_forward(const admm_tv_desc* dp, const float* xin, const float* kern,
 
     int R = env_int("ADMM_PASSA_R", 0);
     if (R <= 0) {
-        // rows per strip: as tall as possible while keeping >= ~3 waves per SIMD of strips in flight
+        // rows per strip (measured on MI355X, tools/sweep.py): 8 for full-wave rows (W >= 1024),
+        // 16 below; halve while there are fewer than ~3 waves per SIMD of strips
         const int L = std::min(64, N / (N >= 1024 ? 16 : N >= 64 ? 8 : N >= 16 ? 4 : 2));
-        const long long want = 3LL * 1024 * 64 / L;  // strips for ~3 waves/SIMD over 256 CUs
-        R = 16;
+        const long long want = 3LL * 1024 * 64 / L;
+        R = N >= 512 ? 8 : 16;
         while (R > 2 && rows / R < want) R /= 2;
     }
     if (R > H) R = H;

@@ -231,16 +231,30 @@ __global__ void __launch_bounds__(256) k_row_c2r(const cf* __restrict__ spec, fl
 // pass B: column FFT -> multiply -> column IFFT, in place, C columns per block
 // MODE 0: real Wiener factor fcT;  MODE 1: complex multiplier mT (PSF transpose)
 // ---------------------------------------------------------------------------
+// min waves per SIMD for pass B: as many blocks per CU as the LDS admits (<= 2)
+constexpr int pb_minw(int nt, size_t lds) {
+    return (nt / 64 * ((160 * 1024) / lds >= 2 ? 2 : 1) + 3) / 4 > 4 ? 4
+                                                                      : (nt / 64 * ((160 * 1024) / lds >= 2 ? 2 : 1) + 3) / 4;
+}
+
 template <int H, int C> struct ColGeom {
     static constexpr int E = RowCfg<H>::E, L = H / E, NT = C * L;
     static constexpr int SYNC = 1;
     static constexpr size_t lds_bytes() { return sizeof(cf) * (H + (size_t)H * C); }
 };
 
+// XCD-aware remap (T1): blocks are dealt round-robin over the 8 XCDs; give each XCD a
+// contiguous range of logical ids so neighbouring column blocks (which share 128-B
+// lines of every row) run on the same L2 at about the same time.  Bijective for any nb.
+__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
+    const unsigned x = b & 7u, i = b >> 3, q = nb >> 3, r = nb & 7u;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 template <int H, int C, int MODE>
-__global__ void __launch_bounds__(C * (H / RowCfg<H>::E)) k_pass_b(cf* __restrict__ spec, const float* __restrict__ fcT,
-                                                              const cf* __restrict__ mT, const cf* __restrict__ twH_g,
-                                                              int N, int colblocks) {
+__global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCfg<H>::E), sizeof(cf) * (H + (size_t)H * C)))
+    k_pass_b(cf* __restrict__ spec, const float* __restrict__ fcT, const cf* __restrict__ mT,
+             const cf* __restrict__ twH_g, int N, int colblocks) {
     using G = ColGeom<H, C>;
     constexpr int E = G::E, L = G::L;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -249,12 +263,29 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E)) k_pass_b(cf* __restric
     load_tw(tw, twH_g, H);
     const int tid = threadIdx.x;
     const int c = tid % C, t = tid / C;
-    const int p = blockIdx.x / colblocks, cb = blockIdx.x % colblocks;
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int p = lb / colblocks, cb = lb % colblocks;
     const int col = cb * C + c;
-    cf* base = spec + (size_t)p * H * N + col;
+    // one plane of the spectrum = H*N*8 bytes (< 4 GiB); element (row, col) at (row*N + col)*8
+    const rsrc_t rs = make_rsrc(spec + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+    const int voff = (t * N + col) * (int)sizeof(cf);
+    const int sstep = L * N * (int)sizeof(cf);
     cf v[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) v[j] = base[(size_t)(t + L * j) * N];
+    for (int j = 0; j < E; ++j) v[j] = bload_cf(rs, voff, j * sstep);
+    // multipliers for this column, prefetched with the data (L2-resident tables)
+    using MT = typename std::conditional<MODE == 0, float, cf>::type;
+    MT m[E];
+    {
+        const rsrc_t rm = MODE == 0 ? make_rsrc(fcT, (unsigned)((size_t)(N + 1) * H * sizeof(float)))
+                                    : make_rsrc(mT, (unsigned)((size_t)(N + 1) * H * sizeof(cf)));
+        const int mo = (col * H + t) * (int)sizeof(MT);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            if constexpr (MODE == 0) m[j] = bload_f(rm, mo, j * L * (int)sizeof(float));
+            else m[j] = bload_cf(rm, mo, j * L * (int)sizeof(cf));
+        }
+    }
     __syncthreads();
     ColBuf<C> buf{data + c};
     fft<H, L, -1, 1, 1>(v, buf, tw, t);
@@ -263,33 +294,34 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E)) k_pass_b(cf* __restric
 #pragma unroll
         for (int j = 0; j < E; ++j) buf.at(t + L * j) = v[j];
         __syncthreads();
-    }
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        const int ky = t + L * j;
         if (col == 0) {
-            const cf q = cconj(buf.at((H - ky) & (H - 1)));
-            if constexpr (MODE == 0) {
-                const float f0 = fcT[ky], fn = fcT[(size_t)N * H + ky];
-                const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
-                v[j] = mkc(a * v[j].x + b * q.x, a * v[j].y + b * q.y);
-            } else {
-                const cf m0 = mT[ky], mn = mT[(size_t)N * H + ky];
-                const cf a = mkc(0.5f * (m0.x + mn.x), 0.5f * (m0.y + mn.y));
-                const cf b = mkc(0.5f * (m0.x - mn.x), 0.5f * (m0.y - mn.y));
-                v[j] = cadd(cmul(v[j], a), cmul(q, b));
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int ky = t + L * j;
+                const cf q = cconj(buf.at((H - ky) & (H - 1)));
+                if constexpr (MODE == 0) {
+                    const float f0 = m[j], fn = fcT[(size_t)N * H + ky];
+                    const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
+                    v[j] = mkc(fmaf(a, v[j].x, b * q.x), fmaf(a, v[j].y, b * q.y));
+                } else {
+                    const cf m0 = m[j], mn = mT[(size_t)N * H + ky];
+                    const cf a = mkc(0.5f * (m0.x + mn.x), 0.5f * (m0.y + mn.y));
+                    const cf b = mkc(0.5f * (m0.x - mn.x), 0.5f * (m0.y - mn.y));
+                    v[j] = cadd(cmul(v[j], a), cmul(q, b));
+                }
             }
-        } else {
-            if constexpr (MODE == 0) {
-                v[j] = cscale(v[j], fcT[(size_t)col * H + ky]);
-            } else {
-                v[j] = cmul(v[j], mT[(size_t)col * H + ky]);
-            }
+        }
+    }
+    if (col != 0) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            if constexpr (MODE == 0) v[j] = cscale(v[j], m[j]);
+            else v[j] = cmul(v[j], m[j]);
         }
     }
     fft<H, L, +1, 1, 1>(v, buf, tw, t);
 #pragma unroll
-    for (int j = 0; j < E; ++j) base[(size_t)(t + L * j) * N] = v[j];
+    for (int j = 0; j < E; ++j) bstore_cf(rs, voff, j * sstep, v[j]);
 }
 
 // ---------------------------------------------------------------------------
@@ -400,7 +432,7 @@ __global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
                 const cf bb = bimg[rm + t + L * j];
                 const float v0 = (wxp[j].x - wxp[j].y) + (wyp[j].x - wyc[j].x);
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
-                r[j] = mkc(bb.x + rho * v0, bb.y + rho * v1);
+                r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
             }
             RowXf<N>::r2c(r, buf, tw, t);
 #pragma unroll
@@ -501,10 +533,10 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
             const float xl = (t == 0) ? sh[(j - 1) & (E - 1)].x : sh[j].x;
             const float ax0 = (xc[j].x - xl) + ux.x, ax1 = (xc[j].y - xc[j].x) + ux.y;
             const float ay0 = (xc[j].x - xp[j].x) + uy.x, ay1 = (xc[j].y - xp[j].y) + uy.y;
-            sx[j].x += ax0 * ax0;
-            sx[j].y += ax1 * ax1;
-            sy[j].x += ay0 * ay0;
-            sy[j].y += ay1 * ay1;
+            sx[j].x = fmaf(ax0, ax0, sx[j].x);
+            sx[j].y = fmaf(ax1, ax1, sx[j].y);
+            sy[j].x = fmaf(ay0, ay0, sy[j].x);
+            sy[j].y = fmaf(ay1, ay1, sy[j].y);
         }
     }
     cf* px = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 0) * H * W) + (size_t)g * N;

@@ -27,9 +27,17 @@ typedef float2 cf;
 __device__ __forceinline__ cf mkc(float r, float i) { cf z; z.x = r; z.y = i; return z; }
 __device__ __forceinline__ cf cadd(cf a, cf b) { return mkc(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ cf csub(cf a, cf b) { return mkc(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ cf cmul(cf a, cf b) { return mkc(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+// Complex products with explicit fused multiply-adds.  The library is compiled with
+// -ffp-contract=off, so every rounding is spelled out here and identical in every
+// inlined copy (a row transformed as a halo row rounds exactly like the same row
+// transformed as an interior row: results do not depend on strip boundaries).
+__device__ __forceinline__ cf cmul(cf a, cf b) {
+    return mkc(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
+}
 // a * conj(b)
-__device__ __forceinline__ cf cmulc(cf a, cf b) { return mkc(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y); }
+__device__ __forceinline__ cf cmulc(cf a, cf b) {
+    return mkc(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -(a.x * b.y)));
+}
 __device__ __forceinline__ cf cconj(cf a) { return mkc(a.x, -a.y); }
 __device__ __forceinline__ cf cscale(cf a, float s) { return mkc(a.x * s, a.y * s); }
 // multiply by DIR*i  (DIR = -1: -i, forward;  DIR = +1: +i, inverse)
@@ -75,10 +83,30 @@ template <int R, int DIR, int K> __device__ __forceinline__ cf tw_mul(cf a) {
         constexpr float cr = ConstTw<R, DIR, K>::re, ci = ConstTw<R, DIR, K>::im;
         constexpr float sr = cr > 0 ? 1.f : -1.f, si = ci > 0 ? 1.f : -1.f;
         // (sr + i si) h * (x + i y) = h (sr x - si y) + i h (sr y + si x)
-        return mkc(h * (sr * a.x - si * a.y), h * (sr * a.y + si * a.x));
+        return mkc(h * (sr * a.x - si * a.y), h * (sr * a.y + si * a.x));  // sr, si = +-1: exact
     } else {
         return cmul(a, mkc(ConstTw<R, DIR, K>::re, ConstTw<R, DIR, K>::im));
     }
+}
+
+// ---------------------------------------------------------------------------
+// buffer-resource memory access (T8): 32-bit per-lane offset + wave-uniform SGPR
+// offset, so strided per-lane streams need one VGPR instead of one 64-bit address
+// per element.  Descriptors must be built from wave-uniform values.
+// ---------------------------------------------------------------------------
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ cf bload_cf(rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore_cf(rsrc_t r, int voff, int soff, cf v) {
+    typedef decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)) V2;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, voff, soff, 0);
+}
+__device__ __forceinline__ float bload_f(rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
 // ---------------------------------------------------------------------------
