@@ -18,8 +18,8 @@
  *    least admm_tv_workspace_size() bytes and 256-byte aligned.
  *  - Return value: 0 on success, a negative ADMM_TV_E* code otherwise.  Error
  *    classes mirror the reference's exceptions: the Python
- *    wrapper raises ValueError for ADMM_TV_EINVAL_RANK and RuntimeError
- *    otherwise.
+ *    wrapper validates shapes first (ValueError / IndexError / RuntimeError as
+ *    the reference raises them) and maps any native error to RuntimeError.
  */
 #ifndef ADMM_TV_H
 #define ADMM_TV_H
@@ -72,6 +72,29 @@ int admm_tv_workspace_size(const admm_tv_desc* desc, size_t* bytes);
 int admm_tv_forward(const admm_tv_desc* desc, const float* xin, const float* kern,
                     const float* lambda_dev, const float* rho_dev, float* out,
                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- autograd
+ * Replaces the reference's implicit autograd through the unrolled loop
+ * (deconv.py:103-115 differentiated by PyTorch).
+ *
+ * Training forward: same result as admm_tv_forward, and additionally stores, for
+ * every iteration k, a_k = D x_k + u_{k-1} (x and y images) and, for iso, the
+ * per-pixel norms N_k in `hist` (admm_tv_history_size bytes; kept by the caller
+ * until the backward).                                                          */
+int admm_tv_history_size(const admm_tv_desc* desc, size_t* bytes);
+int admm_tv_forward_train(const admm_tv_desc* desc, const float* xin, const float* kern,
+                          const float* lambda_dev, const float* rho_dev, float* out,
+                          void* hist, size_t hist_bytes,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
+/* Backward: given gout = dL/dx_K and the training history, writes dL/dxin
+ * (gxin, may be NULL), dL/dlambda and dL/drho (glam, grho: device scalars, both or
+ * neither).  The PSF gradient is not produced by this version.                  */
+int admm_tv_backward_workspace_size(const admm_tv_desc* desc, size_t* bytes);
+int admm_tv_backward(const admm_tv_desc* desc, const float* kern, const float* lambda_dev,
+                     const float* rho_dev, const float* gout, const void* hist, size_t hist_bytes,
+                     float* gxin, float* glam, float* grho,
+                     void* workspace, size_t workspace_bytes, void* stream);
 
 /* b = H_t(xin): the reference's circular PSF "adjoint" (a centred circular
  * CONVOLUTION, deconv.py:86-101), via the same FFT passes.  Exposed for tests. */

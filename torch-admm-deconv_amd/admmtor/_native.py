@@ -26,6 +26,10 @@ EXPORTED = (
     "admm_tv_workspace_size",
     "admm_tv_forward",
     "admm_tv_psf_transpose",
+    "admm_tv_history_size",
+    "admm_tv_forward_train",
+    "admm_tv_backward_workspace_size",
+    "admm_tv_backward",
     "admm_tv_profile_enable",
     "admm_tv_profile_reset",
     "admm_tv_profile_read",
@@ -84,6 +88,14 @@ def load() -> ctypes.CDLL:
         L.admm_tv_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
         L.admm_tv_forward.restype = ctypes.c_int
         L.admm_tv_forward.argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp]
+        L.admm_tv_history_size.restype = ctypes.c_int
+        L.admm_tv_history_size.argtypes = [dp, ctypes.POINTER(sz)]
+        L.admm_tv_forward_train.restype = ctypes.c_int
+        L.admm_tv_forward_train.argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp]
+        L.admm_tv_backward_workspace_size.restype = ctypes.c_int
+        L.admm_tv_backward_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
+        L.admm_tv_backward.restype = ctypes.c_int
+        L.admm_tv_backward.argtypes = [dp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, sz, vp]
         L.admm_tv_psf_transpose.restype = ctypes.c_int
         L.admm_tv_psf_transpose.argtypes = [dp, vp, vp, vp, vp, sz, vp]
         L.admm_tv_profile_enable.restype = ctypes.c_int
@@ -113,6 +125,18 @@ def desc(B, C, H, W, k, iso, maxit) -> AdmmTvDesc:
 def workspace_size(d: AdmmTvDesc) -> int:
     n = ctypes.c_size_t(0)
     check(load().admm_tv_workspace_size(ctypes.byref(d), ctypes.byref(n)))
+    return int(n.value)
+
+
+def history_size(d: AdmmTvDesc) -> int:
+    n = ctypes.c_size_t(0)
+    check(load().admm_tv_history_size(ctypes.byref(d), ctypes.byref(n)))
+    return int(n.value)
+
+
+def backward_workspace_size(d: AdmmTvDesc) -> int:
+    n = ctypes.c_size_t(0)
+    check(load().admm_tv_backward_workspace_size(ctypes.byref(d), ctypes.byref(n)))
     return int(n.value)
 
 

@@ -1,0 +1,399 @@
+// admm_backward.hpp -- reverse pass of the unrolled ADMM-TV iteration (gfx950).
+//
+// Forward iteration k = 1..K (training mode keeps a_k for every k, see pass A):
+//   r_k = b + rho D^T w_{k-1}            w_{k-1} = z_{k-1} - u_{k-1}   (w_0 = u_0 = 0)
+//   x_k = M r_k,  M = F^-1 diag(fc) F    (self-adjoint)
+//   a_k = D x_k + u_{k-1};  z_k = S(a_k; tau);  u_k = a_k - z_k;  w_k = 2 z_k - a_k
+// Reverse step k = K..1, given the adjoints u^_k, w^_k of iteration k's outputs
+// (zero at k = K) and x^_K = dL/dx_K:
+//   r^_k   = M x^_k                                  (pass B, unchanged)
+//   b^    += r^_k
+//   w^_{k-1} = rho D r^_k
+//   rho^  += <D r^_k, w_{k-1}> - <D r^_k, D x_k>     (second term: dM/drho = -M D^T D M)
+//   z^_{k-1} = 2 w^_{k-1} - u^_{k-1},  u^_{k-1} = a^_k
+//   a^_{k-1} = u^_{k-1} - w^_{k-1} + J_S(a_{k-1})^T z^_{k-1};  tau^ += dS/dtau . z^_{k-1}
+//   x^_{k-1} = D^T a^_{k-1}
+// with D x_k = a_k - u_{k-1}.  The spatial stencils and shrink Jacobians are fused into
+// one row pass (k_bwd_pass_a), the same strip/halo structure as the forward pass A.
+// iso: J_S couples planes through the per-pixel norm; Q = sum_{b,c} a z^ is formed by
+// k_bwd_iso_q first (like the forward norm pass).
+#pragma once
+#include "admm_kernels.hpp"
+
+namespace admm {
+
+struct BwdArgs {
+    const cf* sin;        // r^_k row spectra (pass B output)                  [P][H][N]
+    cf* sout;             // x^_{k-1} row spectra (k >= 2)                      [P][H][N]
+    float* bbar;          // b^ accumulator                                    [P][H][W]
+    const float* abx_in;  // a^_k = u^_{k-1}  (k < K)                           [P][H][W]
+    const float* aby_in;
+    float* abx_out;       // a^_{k-1} (k >= 2)
+    float* aby_out;
+    const float* akx;     // a_k      (history slot k-1)
+    const float* aky;
+    const float* apx;     // a_{k-1}  (history slot k-2, k >= 2)
+    const float* apy;
+    const float* np;      // iso: N_{k-1}                                       [2][H][W]
+    const float* qp;      // iso: Q_{k-1} = sum_{b,c} a_{k-1} z^_{k-1}          [2][H][W]
+    const float* lam;
+    const float* rho;
+    float* part;          // per strip: {rho^ partial, tau^ partial}            [nstrips][2]
+    const cf* twW;
+    int H, R;
+    long long nstrips;
+};
+
+// S'(a) contracted with z^: aniso mask, iso block Jacobian (f z^ + 2 a f'(N) Q)
+template <bool ISO>
+__device__ __forceinline__ float shrink_vjp(float a, float zb, float tau, float n, float q) {
+    if constexpr (ISO) {
+        const float s = sqrtf(n + 1e-15f);
+        const float d = s + 1e-15f;
+        const float f = 1.f - tau / d;
+        if (!(f > 0.f)) return 0.f;
+        const float fp = tau / (d * d) * (0.5f / s);  // df/dN
+        return fmaf(f, zb, 2.f * a * fp * q);
+    } else {
+        return (fabsf(a) > tau) ? zb : 0.f;
+    }
+}
+// dS/dtau . z^ (aniso only; iso's tau term is summed per pixel in k_bwd_iso_q)
+__device__ __forceinline__ float soft_dtau(float a, float zb, float tau) {
+    return (fabsf(a) > tau) ? (a > 0.f ? -zb : zb) : 0.f;  // -sign(a) z^ on the active set
+}
+
+template <int N, bool ISO, bool LASTK, bool FIRSTK>
+__global__ void __launch_bounds__(256) k_bwd_pass_a(BwdArgs a) {
+    using G = RowKernelGeom<N>;
+    constexpr int E = G::E, L = G::L, W = G::W;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, a.twW, W);
+    __syncthreads();
+    const int sgl = threadIdx.x / L, t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * G::SG + sgl;
+    if (strip >= a.nstrips) return;
+    const int H = a.H, R = a.R;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    const float rho = a.rho[0];
+    const float tau = a.lam[0] / rho;
+
+    const cf* sp = a.sin + (size_t)p * H * N;
+    cf* so = a.sout + (size_t)p * H * N;
+    const size_t poff = (size_t)p * H * W;
+    auto img = [&](const float* base) { return reinterpret_cast<const cf*>(base + poff); };
+    cf* bb = reinterpret_cast<cf*>(a.bbar + poff);
+    const cf* abxi = LASTK ? nullptr : img(a.abx_in);
+    const cf* abyi = LASTK ? nullptr : img(a.aby_in);
+    cf* abxo = FIRSTK ? nullptr : reinterpret_cast<cf*>(a.abx_out + poff);
+    cf* abyo = FIRSTK ? nullptr : reinterpret_cast<cf*>(a.aby_out + poff);
+    const cf* akx = img(a.akx);
+    const cf* aky = img(a.aky);
+    const cf* apx = FIRSTK ? nullptr : img(a.apx);
+    const cf* apy = FIRSTK ? nullptr : img(a.apy);
+    const cf* npx = reinterpret_cast<const cf*>(a.np);
+    const cf* npy = reinterpret_cast<const cf*>(a.np + (size_t)H * W);
+    const cf* qpx = reinterpret_cast<const cf*>(a.qp);
+    const cf* qpy = reinterpret_cast<const cf*>(a.qp + (size_t)H * W);
+
+    float rho_acc = 0.f, tau_acc = 0.f;
+    cf rprev[E], rcur[E], abxp[E], abyp[E];
+    {
+        const int g = (i0 - 1 + H) & (H - 1);
+#pragma unroll
+        for (int j = 0; j < E; ++j) rprev[j] = sp[(size_t)g * N + t + L * j];
+        RowXf<N>::c2r(rprev, buf, tw, t);
+    }
+    for (int rr = 0; rr <= R; ++rr) {
+        const int g = (i0 + rr) & (H - 1);
+        const size_t ro = (size_t)g * N;
+#pragma unroll
+        for (int j = 0; j < E; ++j) rcur[j] = sp[ro + t + L * j];
+        RowXf<N>::c2r(rcur, buf, tw, t);
+
+        // ---- y direction at row g
+        cf abyc[E];
+        {
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int i = (int)ro + t + L * j;
+                const float d0 = rcur[j].x - rprev[j].x, d1 = rcur[j].y - rprev[j].y;  // Dy r^
+                cf ap = mkc(0.f, 0.f), npv = mkc(0.f, 0.f);
+                if constexpr (!FIRSTK) {
+                    ap = apy[i];
+                    if constexpr (ISO) npv = npy[i];
+                }
+                const float zp0 = FIRSTK ? 0.f : shrink_z<ISO>(ap.x, tau, npv.x);
+                const float zp1 = FIRSTK ? 0.f : shrink_z<ISO>(ap.y, tau, npv.y);
+                if (rr < R) {
+                    // rho^ += Dy r^ . (w_{k-1} - Dy x_k),  w = 2z - a,  Dy x_k = a_k - u_{k-1} = a_k - a_p + z_p
+                    const cf ak = aky[i];
+                    const float e0 = (2.f * zp0 - ap.x) - (ak.x - ap.x + zp0);
+                    const float e1 = (2.f * zp1 - ap.y) - (ak.y - ap.y + zp1);
+                    rho_acc = fmaf(d0, e0, fmaf(d1, e1, rho_acc));
+                }
+                if constexpr (!FIRSTK) {
+                    const cf ub = LASTK ? mkc(0.f, 0.f) : abyi[i];
+                    const float wb0 = rho * d0, wb1 = rho * d1;
+                    const float zb0 = 2.f * wb0 - ub.x, zb1 = 2.f * wb1 - ub.y;
+                    cf q = mkc(0.f, 0.f);
+                    if constexpr (ISO) q = qpy[i];
+                    abyc[j] = mkc(ub.x - wb0 + shrink_vjp<ISO>(ap.x, zb0, tau, npv.x, q.x),
+                                  ub.y - wb1 + shrink_vjp<ISO>(ap.y, zb1, tau, npv.y, q.y));
+                    if constexpr (!ISO) {
+                        if (rr < R) tau_acc += soft_dtau(ap.x, zb0, tau) + soft_dtau(ap.y, zb1, tau);
+                    }
+                }
+            }
+            if constexpr (!FIRSTK) {
+                if (rr < R) {
+#pragma unroll
+                    for (int j = 0; j < E; ++j) abyo[ro + t + L * j] = abyc[j];
+                }
+            }
+        }
+        // ---- b^ += r^ (row g)
+        if (rr < R) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                cf v = rcur[j];
+                if constexpr (!LASTK) {
+                    const cf o = bb[ro + t + L * j];
+                    v = mkc(o.x + v.x, o.y + v.y);
+                }
+                bb[ro + t + L * j] = v;
+            }
+        }
+        // ---- finalize x^_{k-1} at row g-1: D^T a^ = (a^x[j] - a^x[j+1]) + (a^y[g-1] - a^y[g])
+        if constexpr (!FIRSTK) {
+            if (rr >= 1) {
+                const int gm = (g - 1 + H) & (H - 1);
+                const size_t rm = (size_t)gm * N;
+                cf r[E], sh[E];
+#pragma unroll
+                for (int j = 0; j < E; ++j) sh[j].x = __shfl(abxp[j].x, (t + 1) & (L - 1), L);
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    const float ar = (t == L - 1) ? sh[(j + 1) & (E - 1)].x : sh[j].x;
+                    r[j] = mkc((abxp[j].x - abxp[j].y) + (abyp[j].x - abyc[j].x),
+                               (abxp[j].y - ar) + (abyp[j].y - abyc[j].y));
+                }
+                RowXf<N>::r2c(r, buf, tw, t);
+#pragma unroll
+                for (int j = 0; j < E; ++j) so[rm + t + L * j] = r[j];
+            }
+        }
+        // ---- x direction at row g
+        if (rr < R) {
+            cf sh[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) sh[j].x = __shfl(rcur[j].y, (t - 1) & (L - 1), L);
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int i = (int)ro + t + L * j;
+                const float rl = (t == 0) ? sh[(j - 1) & (E - 1)].x : sh[j].x;
+                const float d0 = rcur[j].x - rl, d1 = rcur[j].y - rcur[j].x;  // Dx r^
+                cf ap = mkc(0.f, 0.f), npv = mkc(0.f, 0.f);
+                if constexpr (!FIRSTK) {
+                    ap = apx[i];
+                    if constexpr (ISO) npv = npx[i];
+                }
+                const float zp0 = FIRSTK ? 0.f : shrink_z<ISO>(ap.x, tau, npv.x);
+                const float zp1 = FIRSTK ? 0.f : shrink_z<ISO>(ap.y, tau, npv.y);
+                const cf ak = akx[i];
+                const float e0 = (2.f * zp0 - ap.x) - (ak.x - ap.x + zp0);
+                const float e1 = (2.f * zp1 - ap.y) - (ak.y - ap.y + zp1);
+                rho_acc = fmaf(d0, e0, fmaf(d1, e1, rho_acc));
+                if constexpr (!FIRSTK) {
+                    const cf ub = LASTK ? mkc(0.f, 0.f) : abxi[i];
+                    const float wb0 = rho * d0, wb1 = rho * d1;
+                    const float zb0 = 2.f * wb0 - ub.x, zb1 = 2.f * wb1 - ub.y;
+                    cf q = mkc(0.f, 0.f);
+                    if constexpr (ISO) q = qpx[i];
+                    abxp[j] = mkc(ub.x - wb0 + shrink_vjp<ISO>(ap.x, zb0, tau, npv.x, q.x),
+                                  ub.y - wb1 + shrink_vjp<ISO>(ap.y, zb1, tau, npv.y, q.y));
+                    if constexpr (!ISO) tau_acc += soft_dtau(ap.x, zb0, tau) + soft_dtau(ap.y, zb1, tau);
+                }
+            }
+            if constexpr (!FIRSTK) {
+#pragma unroll
+                for (int j = 0; j < E; ++j) abxo[ro + t + L * j] = abxp[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            if constexpr (!FIRSTK) abyp[j] = abyc[j];
+            rprev[j] = rcur[j];
+        }
+    }
+    // per-strip partial sums (fixed-order butterfly over the sub-group's lanes)
+#pragma unroll
+    for (int o = L / 2; o >= 1; o >>= 1) {
+        rho_acc += __shfl_xor(rho_acc, o, L);
+        tau_acc += __shfl_xor(tau_acc, o, L);
+    }
+    if (t == 0) {
+        a.part[2 * strip + 0] = rho_acc;
+        a.part[2 * strip + 1] = tau_acc;
+    }
+}
+
+// iso: Q_{k-1}[pixel] = sum over planes of a_{k-1} z^_{k-1}, z^ = 2 rho D r^_k - a^_k;
+// per (plane group, row) partial sums, reduced by k_iso_reduce.
+struct BwdIsoArgs {
+    const cf* sin;       // r^_k row spectra
+    const float* abx_in; // a^_k (k < K)
+    const float* aby_in;
+    const float* apx;    // a_{k-1}
+    const float* apy;
+    const float* rho;
+    float* partial;      // [ngroups][2][H][W]
+    const cf* twW;
+    int P, H, ppg;
+    long long nitems;
+};
+
+template <int N, bool LASTK>
+__global__ void __launch_bounds__(256) k_bwd_iso_q(BwdIsoArgs a) {
+    using G = RowKernelGeom<N>;
+    constexpr int E = G::E, L = G::L, W = G::W;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, a.twW, W);
+    __syncthreads();
+    const int sgl = threadIdx.x / L, t = threadIdx.x % L;
+    const long long item = (long long)blockIdx.x * G::SG + sgl;
+    if (item >= a.nitems) return;
+    const int H = a.H;
+    const int g = (int)(item % H);
+    const int grp = (int)(item / H);
+    const int gm = (g - 1 + H) & (H - 1);
+    RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    const float rho = a.rho[0];
+    cf qx[E], qy[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) qx[j] = qy[j] = mkc(0.f, 0.f);
+    const int p1 = min(a.P, (grp + 1) * a.ppg);
+    for (int p = grp * a.ppg; p < p1; ++p) {
+        const cf* sp = a.sin + (size_t)p * H * N;
+        cf rp[E], rc[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            rp[j] = sp[(size_t)gm * N + t + L * j];
+            rc[j] = sp[(size_t)g * N + t + L * j];
+        }
+        RowXf<N>::c2r(rp, buf, tw, t);
+        RowXf<N>::c2r(rc, buf, tw, t);
+        const size_t ro = (size_t)p * H * N + (size_t)g * N;
+        const cf* abx = reinterpret_cast<const cf*>(a.abx_in);
+        const cf* aby = reinterpret_cast<const cf*>(a.aby_in);
+        const cf* apx = reinterpret_cast<const cf*>(a.apx);
+        const cf* apy = reinterpret_cast<const cf*>(a.apy);
+        cf sh[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) sh[j].x = __shfl(rc[j].y, (t - 1) & (L - 1), L);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const float rl = (t == 0) ? sh[(j - 1) & (E - 1)].x : sh[j].x;
+            const cf ubx = LASTK ? mkc(0.f, 0.f) : abx[ro + t + L * j];
+            const cf uby = LASTK ? mkc(0.f, 0.f) : aby[ro + t + L * j];
+            const cf ax = apx[ro + t + L * j], ay = apy[ro + t + L * j];
+            const float zx0 = 2.f * rho * (rc[j].x - rl) - ubx.x, zx1 = 2.f * rho * (rc[j].y - rc[j].x) - ubx.y;
+            const float zy0 = 2.f * rho * (rc[j].x - rp[j].x) - uby.x, zy1 = 2.f * rho * (rc[j].y - rp[j].y) - uby.y;
+            qx[j].x = fmaf(ax.x, zx0, qx[j].x);
+            qx[j].y = fmaf(ax.y, zx1, qx[j].y);
+            qy[j].x = fmaf(ay.x, zy0, qy[j].x);
+            qy[j].y = fmaf(ay.y, zy1, qy[j].y);
+        }
+    }
+    cf* px = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 0) * H * W) + (size_t)g * N;
+    cf* py = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 1) * H * W) + (size_t)g * N;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        px[t + L * j] = qx[j];
+        py[t + L * j] = qy[j];
+    }
+}
+
+// iso tau^: sum over pixels of -Q / (s + eps) where f > 0 (dz/dtau = -a / (s + eps));
+// one partial per block, fixed order.
+__global__ void k_iso_tau_partial(const float* __restrict__ q, const float* __restrict__ n,
+                                  const float* __restrict__ lam, const float* __restrict__ rho,
+                                  float* __restrict__ part, long long count) {
+    __shared__ float red[256];
+    const float tau = lam[0] / rho[0];
+    float acc = 0.f;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+         i += (long long)gridDim.x * blockDim.x) {
+        const float s = sqrtf(n[i] + 1e-15f), d = s + 1e-15f;
+        if (1.f - tau / d > 0.f) acc += -q[i] / d;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// final scalars: tau^ = sum of partials, rho^ = sum + tau^ * (-lam / rho^2), lam^ = tau^ / rho
+// (single block, fixed order -> deterministic)
+__global__ void k_bwd_scalars(const float* __restrict__ part, long long nstrip_parts, const float* __restrict__ tpart,
+                              int ntp, const float* __restrict__ lam, const float* __restrict__ rho,
+                              float* __restrict__ glam, float* __restrict__ grho) {
+    __shared__ double r1[256], r2[256];
+    double sr = 0.0, st = 0.0;
+    for (long long i = threadIdx.x; i < nstrip_parts; i += blockDim.x) {
+        sr += part[2 * i + 0];
+        st += part[2 * i + 1];
+    }
+    for (int i = threadIdx.x; i < ntp; i += blockDim.x) st += tpart[i];
+    r1[threadIdx.x] = sr;
+    r2[threadIdx.x] = st;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+            r2[threadIdx.x] += r2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double l = lam[0], r = rho[0];
+        const double tb = r2[0];
+        glam[0] = (float)(tb / r);
+        grho[0] = (float)(r1[0] - tb * l / (r * r));
+    }
+}
+
+// accumulate per-iteration scalar partials into a running [2] (rho^, tau^) pair in fp64-free fixed order
+__global__ void k_accum_parts(const float* __restrict__ part, long long n, float* __restrict__ acc) {
+    // acc[0..1] += sum(part[2i], part[2i+1]); one block
+    __shared__ float r1[256], r2[256];
+    float sr = 0.f, st = 0.f;
+    for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+        sr += part[2 * i];
+        st += part[2 * i + 1];
+    }
+    r1[threadIdx.x] = sr;
+    r2[threadIdx.x] = st;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+            r2[threadIdx.x] += r2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        acc[0] += r1[0];
+        acc[1] += r2[0];
+    }
+}
+
+}  // namespace admm

@@ -13,7 +13,7 @@
 #include <type_traits>
 #include <vector>
 
-#include "admm_kernels.hpp"
+#include "admm_backward.hpp"
 #include "admm_tv.h"
 
 using namespace admm;
@@ -160,28 +160,59 @@ template <int N> struct RowOps {
         hipLaunchKernelGGL(k_row_c2r<N>, dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, spec, img, twW, rows);
         return launch_check("k_row_c2r");
     }
-    static int pass_a(const PassAArgs& a, bool iso, bool first, hipStream_t s) {
+    template <bool ISO, bool FIRST, bool HIST> static void pa(const PassAArgs& a, unsigned nb, hipStream_t s) {
+        hipLaunchKernelGGL((k_pass_a<N, ISO, FIRST, HIST>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+    }
+    static int pass_a(const PassAArgs& a, bool iso, bool first, bool hist, hipStream_t s) {
         const unsigned nb = blocks(a.nstrips);
-        if (iso) {
-            if (first)
-                hipLaunchKernelGGL((k_pass_a<N, true, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
-            else
-                hipLaunchKernelGGL((k_pass_a<N, true, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
-        } else {
-            if (first)
-                hipLaunchKernelGGL((k_pass_a<N, false, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
-            else
-                hipLaunchKernelGGL((k_pass_a<N, false, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        const int sel = (iso ? 4 : 0) | (first ? 2 : 0) | (hist ? 1 : 0);
+        switch (sel) {
+            case 0: pa<false, false, false>(a, nb, s); break;
+            case 1: pa<false, false, true>(a, nb, s); break;
+            case 2: pa<false, true, false>(a, nb, s); break;
+            case 3: pa<false, true, true>(a, nb, s); break;
+            case 4: pa<true, false, false>(a, nb, s); break;
+            case 5: pa<true, false, true>(a, nb, s); break;
+            case 6: pa<true, true, false>(a, nb, s); break;
+            default: pa<true, true, true>(a, nb, s); break;
         }
         return launch_check("k_pass_a");
     }
-    static int iso_norm(const IsoArgs& a, bool first, hipStream_t s) {
+    static int iso_norm(const IsoArgs& a, bool first, bool hist, hipStream_t s) {
         const unsigned nb = blocks(a.nitems);
         if (first)
-            hipLaunchKernelGGL((k_iso_norm<N, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+            hipLaunchKernelGGL((k_iso_norm<N, true, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        else if (hist)
+            hipLaunchKernelGGL((k_iso_norm<N, false, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         else
-            hipLaunchKernelGGL((k_iso_norm<N, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+            hipLaunchKernelGGL((k_iso_norm<N, false, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         return launch_check("k_iso_norm");
+    }
+    template <bool ISO, bool LASTK, bool FIRSTK> static void bpa(const BwdArgs& a, unsigned nb, hipStream_t s) {
+        hipLaunchKernelGGL((k_bwd_pass_a<N, ISO, LASTK, FIRSTK>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+    }
+    static int bwd_pass_a(const BwdArgs& a, bool iso, bool lastk, bool firstk, hipStream_t s) {
+        const unsigned nb = blocks(a.nstrips);
+        const int sel = (iso ? 4 : 0) | (lastk ? 2 : 0) | (firstk ? 1 : 0);
+        switch (sel) {
+            case 0: bpa<false, false, false>(a, nb, s); break;
+            case 1: bpa<false, false, true>(a, nb, s); break;
+            case 2: bpa<false, true, false>(a, nb, s); break;
+            case 3: bpa<false, true, true>(a, nb, s); break;
+            case 4: bpa<true, false, false>(a, nb, s); break;
+            case 5: bpa<true, false, true>(a, nb, s); break;
+            case 6: bpa<true, true, false>(a, nb, s); break;
+            default: bpa<true, true, true>(a, nb, s); break;
+        }
+        return launch_check("k_bwd_pass_a");
+    }
+    static int bwd_iso_q(const BwdIsoArgs& a, bool lastk, hipStream_t s) {
+        const unsigned nb = blocks(a.nitems);
+        if (lastk)
+            hipLaunchKernelGGL((k_bwd_iso_q<N, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        else
+            hipLaunchKernelGGL((k_bwd_iso_q<N, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        return launch_check("k_bwd_iso_q");
     }
 };
 
@@ -208,9 +239,12 @@ template <int H, int C> int pass_b_hc(cf* spec, const float* fcT, const cf* mT, 
     if (mode == 0) {
         if (int e = set_lds(k_pass_b<H, C, 0>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, fcT, mT, twH, N, colblocks);
-    } else {
+    } else if (mode == 1) {
         if (int e = set_lds(k_pass_b<H, C, 1>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, fcT, mT, twH, N, colblocks);
+    } else {
+        if (int e = set_lds(k_pass_b<H, C, 2>, G::lds_bytes())) return e;
+        hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, fcT, mT, twH, N, colblocks);
     }
     return launch_check("k_pass_b");
 }
@@ -278,6 +312,180 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
     return 0;
 }
 
+int strip_rows(int H, int N, long long rows) {
+    int R = env_int("ADMM_PASSA_R", 0);
+    if (R <= 0) {
+        // rows per strip (measured on MI355X, tools/sweep.py): 8 for full-wave rows (W >= 1024),
+        // 16 below; halve while there are fewer than ~3 waves per SIMD of strips
+        const int L = std::min(64, N / (N >= 1024 ? 16 : N >= 64 ? 8 : N >= 16 ? 4 : 2));
+        const long long want = 3LL * 1024 * 64 / L;
+        R = N >= 512 ? 8 : 16;
+        while (R > 2 && rows / R < want) R /= 2;
+    }
+    if (R > H) R = H;
+    return R;
+}
+
+// b = H_t(xin) into `bb` through the FFT passes (scratch: spec)
+int psf_transpose_into(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* xin, float* bb, cf* spec,
+                       int mode, hipStream_t s) {
+    const long long rows = d.B * d.C * d.H;
+    const int H = (int)d.H, N = (int)d.W / 2;
+    cf* twW = at<cf>(ws, Lo.twW);
+    int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(xin, spec, twW, rows, s); });
+    if (e) return e;
+    if ((e = pass_b(H, spec, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), at<cf>(ws, Lo.twH), N, (int)(d.B * d.C), mode, s)))
+        return e;
+    return with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec, bb, twW, rows, s); });
+}
+
+// history (training) storage: a_k for k = 1..K (x and y images), iso norms N_k
+struct Hist {
+    size_t a_slot;     // bytes of one image
+    size_t n_slot;     // bytes of one norm pair [2][H][W]
+    size_t n_off;      // offset of the norm history
+    size_t total;
+};
+Hist make_hist(const admm_tv_desc& d) {
+    Hist h{};
+    const size_t img = (size_t)d.B * d.C * d.H * d.W * sizeof(float);
+    h.a_slot = up(img);
+    h.n_slot = d.iso ? up(2 * (size_t)d.H * d.W * sizeof(float)) : 0;
+    h.n_off = (size_t)d.maxit * 2 * h.a_slot;
+    h.total = h.n_off + (size_t)d.maxit * h.n_slot;
+    return h;
+}
+
+// The forward solver.  hist == nullptr: inference (u ping-pong).  Otherwise training mode:
+// a_k -> hist slot k-1 (x image at 2(k-1), y image at 2(k-1)+1), N_k -> norm slot k-1, and
+// the last iteration's pass A also runs (a_K is needed by the backward).
+int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, const float* lam, const float* rho,
+                float* out, void* ws, size_t ws_bytes, void* hist, hipStream_t s) {
+    const Layout Lo = make_layout(d);
+    if (!ws || ws_bytes < Lo.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
+        return fail(ADMM_TV_EWORKSPACE, "workspace too small or not 256-byte aligned");
+    const long long P = d.B * d.C;
+    const int H = (int)d.H, W = (int)d.W, N = W / 2;
+    const size_t img_bytes = (size_t)P * H * W * sizeof(float);
+    if (d.maxit == 0) {
+        HIPCHK(hipMemsetAsync(out, 0, img_bytes, s));  // the reference returns x = zeros (deconv.py:61,117)
+        return 0;
+    }
+    if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
+    cf* twW = at<cf>(ws, Lo.twW);
+    cf* twH = at<cf>(ws, Lo.twH);
+    float* fcT = at<float>(ws, Lo.fcT);
+    cf* mT = at<cf>(ws, Lo.mT);
+    cf* spec[2] = {at<cf>(ws, Lo.spec[0]), at<cf>(ws, Lo.spec[1])};
+    float* u[4] = {at<float>(ws, Lo.u[0]), at<float>(ws, Lo.u[1]), at<float>(ws, Lo.u[2]), at<float>(ws, Lo.u[3])};
+    const long long rows = P * H;
+    const bool train = hist != nullptr;
+    const Hist Hs = make_hist(d);
+    auto ha = [&](int k, int comp) -> float* {  // a_k image (k >= 1), comp 0 = x, 1 = y
+        return reinterpret_cast<float*>(static_cast<char*>(hist) + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
+    };
+    auto hn = [&](int k) -> float* {  // N_k (k >= 1)
+        return reinterpret_cast<float*>(static_cast<char*>(hist) + Hs.n_off + (size_t)(k - 1) * Hs.n_slot);
+    };
+
+    // b = H_t(xin) once (the reference recomputes it every iteration, deconv.py:104)
+    const float* bimg = xin;
+    if (d.kh > 0) {
+        ProfScope ps(3, s);
+        float* bb = at<float>(ws, Lo.b);
+        if (int e = psf_transpose_into(d, Lo, ws, xin, bb, spec[0], 1, s)) return e;
+        bimg = bb;
+    }
+    {
+        ProfScope ps(3, s);
+        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, spec[0], twW, rows, s); });
+        if (e) return e;
+    }
+    const int R = strip_rows(H, N, rows);
+
+    int cur = 0, uin = 0;  // spec[cur] holds the current r spectra; u[2*uin], u[2*uin+1] = u_x, u_y in
+    for (int it = 1; it <= d.maxit; ++it) {
+        {
+            ProfScope ps(1, s);
+            if (int e = pass_b(H, spec[cur], fcT, mT, twH, N, (int)P, 0, s)) return e;
+        }
+        if (it == d.maxit) {
+            ProfScope ps(3, s);
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec[cur], out, twW, rows, s); });
+            if (e) return e;
+            if (!train) break;
+        }
+        const bool first = (it == 1);
+        const float *uxi, *uyi, *nprev = nullptr;
+        float *uxo, *uyo;
+        if (train) {
+            uxi = first ? nullptr : ha(it - 1, 0);
+            uyi = first ? nullptr : ha(it - 1, 1);
+            uxo = ha(it, 0);
+            uyo = ha(it, 1);
+            if (d.iso && !first) nprev = hn(it - 1);
+        } else {
+            uxi = u[2 * uin];
+            uyi = u[2 * uin + 1];
+            uxo = u[2 * (1 - uin)];
+            uyo = u[2 * (1 - uin) + 1];
+        }
+        const float* nsq = nullptr;
+        if (d.iso) {
+            ProfScope ps(2, s);
+            float* nout = train ? hn(it) : at<float>(ws, Lo.nsq);
+            IsoArgs ia{spec[cur], uxi, uyi, nprev, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
+                       (long long)Lo.ngroups * H};
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::iso_norm(ia, first, train, s); });
+            if (e) return e;
+            const long long n4 = 2LL * H * W / 4;
+            hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                               at<float4>(ws, Lo.part), reinterpret_cast<float4*>(nout), Lo.ngroups, n4);
+            if ((e = launch_check("k_iso_reduce"))) return e;
+            nsq = nout;
+        }
+        {
+            ProfScope ps(0, s);
+            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, rows / R};
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, train, s); });
+            if (e) return e;
+        }
+        cur = 1 - cur;
+        uin = 1 - uin;
+    }
+    return 0;
+}
+
+// backward workspace = forward layout + a^ ping-pong (4 images) + b^ + per-iteration partials
+struct BwdLayout {
+    Layout f;
+    size_t abar[4], bbar, part, tpart, q, total;
+    long long nstrips;
+    int R, ntp;
+};
+BwdLayout make_bwd_layout(const admm_tv_desc& d) {
+    BwdLayout B{};
+    B.f = make_layout(d);
+    const size_t img = (size_t)d.B * d.C * d.H * d.W * sizeof(float);
+    size_t o = B.f.total;
+    auto take = [&](size_t bytes) {
+        size_t at_ = o;
+        o += up(bytes);
+        return at_;
+    };
+    for (int i = 0; i < 4; ++i) B.abar[i] = take(img);
+    B.bbar = take(img);
+    const long long rows = d.B * d.C * d.H;
+    B.R = strip_rows((int)d.H, (int)d.W / 2, rows);
+    B.nstrips = rows / B.R;
+    B.part = take((size_t)std::max(d.maxit, 1) * B.nstrips * 2 * sizeof(float));
+    B.ntp = 256;
+    B.tpart = take((size_t)std::max(d.maxit, 1) * B.ntp * sizeof(float));
+    B.q = take(2 * (size_t)d.H * d.W * sizeof(float));
+    B.total = o;
+    return B;
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -299,95 +507,123 @@ int admm_tv_workspace_size(const admm_tv_desc* d, size_t* bytes) {
 int admm_tv_forward(const admm_tv_desc* dp, const float* xin, const float* kern, const float* lam, const float* rho,
                     float* out, void* ws, size_t ws_bytes, void* stream) {
     if (int e = validate(dp)) return e;
+    if (!xin || !out || !lam || !rho || (dp->kh > 0 && !kern)) return fail(ADMM_TV_EINVAL, "null pointer argument");
+    return run_forward(*dp, xin, kern, lam, rho, out, ws, ws_bytes, nullptr, reinterpret_cast<hipStream_t>(stream));
+}
+
+int admm_tv_history_size(const admm_tv_desc* d, size_t* bytes) {
+    if (int e = validate(d)) return e;
+    if (!bytes) return fail(ADMM_TV_EINVAL, "null bytes");
+    *bytes = make_hist(*d).total;
+    return 0;
+}
+
+int admm_tv_forward_train(const admm_tv_desc* dp, const float* xin, const float* kern, const float* lam,
+                          const float* rho, float* out, void* hist, size_t hist_bytes, void* ws, size_t ws_bytes,
+                          void* stream) {
+    if (int e = validate(dp)) return e;
+    if (!xin || !out || !lam || !rho || (dp->kh > 0 && !kern)) return fail(ADMM_TV_EINVAL, "null pointer argument");
+    if (dp->maxit > 0 && (!hist || hist_bytes < make_hist(*dp).total))
+        return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
+    return run_forward(*dp, xin, kern, lam, rho, out, ws, ws_bytes, dp->maxit > 0 ? hist : nullptr,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+int admm_tv_backward_workspace_size(const admm_tv_desc* d, size_t* bytes) {
+    if (int e = validate(d)) return e;
+    if (!bytes) return fail(ADMM_TV_EINVAL, "null bytes");
+    *bytes = make_bwd_layout(*d).total;
+    return 0;
+}
+
+int admm_tv_backward(const admm_tv_desc* dp, const float* kern, const float* lam, const float* rho,
+                     const float* gout, const void* hist, size_t hist_bytes, float* gxin, float* glam, float* grho,
+                     void* ws, size_t ws_bytes, void* stream) {
+    if (int e = validate(dp)) return e;
     const admm_tv_desc d = *dp;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (!xin || !out || !lam || !rho || (d.kh > 0 && !kern)) return fail(ADMM_TV_EINVAL, "null pointer argument");
-    const Layout Lo = make_layout(d);
-    if (!ws || ws_bytes < Lo.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
+    if (!gout || !lam || !rho || (d.kh > 0 && !kern)) return fail(ADMM_TV_EINVAL, "null pointer argument");
+    const BwdLayout BL = make_bwd_layout(d);
+    const Layout& Lo = BL.f;
+    if (!ws || ws_bytes < BL.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
         return fail(ADMM_TV_EWORKSPACE, "workspace too small or not 256-byte aligned");
     const long long P = d.B * d.C;
-    const int H = (int)d.H, W = (int)d.W, N = W / 2;
+    const int H = (int)d.H, W = (int)d.W, N = W / 2, K = d.maxit;
     const size_t img_bytes = (size_t)P * H * W * sizeof(float);
-    if (d.maxit == 0) {
-        HIPCHK(hipMemsetAsync(out, 0, img_bytes, s));  // the reference returns x = zeros (deconv.py:61,117)
+    if (K == 0) {  // output is identically zero
+        if (gxin) HIPCHK(hipMemsetAsync(gxin, 0, img_bytes, s));
+        if (glam) HIPCHK(hipMemsetAsync(glam, 0, sizeof(float), s));
+        if (grho) HIPCHK(hipMemsetAsync(grho, 0, sizeof(float), s));
         return 0;
     }
+    if (!hist || hist_bytes < make_hist(d).total) return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
+    const Hist Hs = make_hist(d);
+    char* hb = static_cast<char*>(const_cast<void*>(hist));
+    auto ha = [&](int k, int comp) -> const float* {
+        return reinterpret_cast<const float*>(hb + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
+    };
+    auto hn = [&](int k) -> const float* { return reinterpret_cast<const float*>(hb + Hs.n_off + (size_t)(k - 1) * Hs.n_slot); };
     cf* twW = at<cf>(ws, Lo.twW);
     cf* twH = at<cf>(ws, Lo.twH);
     float* fcT = at<float>(ws, Lo.fcT);
     cf* mT = at<cf>(ws, Lo.mT);
     cf* spec[2] = {at<cf>(ws, Lo.spec[0]), at<cf>(ws, Lo.spec[1])};
-    float* u[4] = {at<float>(ws, Lo.u[0]), at<float>(ws, Lo.u[1]), at<float>(ws, Lo.u[2]), at<float>(ws, Lo.u[3])};
+    float* ab[4] = {at<float>(ws, BL.abar[0]), at<float>(ws, BL.abar[1]), at<float>(ws, BL.abar[2]),
+                    at<float>(ws, BL.abar[3])};
+    // b^ accumulates straight into gxin when there is no PSF (x^_in = b^)
+    float* bbar = (d.kh == 0 && gxin) ? gxin : at<float>(ws, BL.bbar);
+    float* part = at<float>(ws, BL.part);
+    float* tpart = at<float>(ws, BL.tpart);
+    float* q = at<float>(ws, BL.q);
     const long long rows = P * H;
-
-    // b = H_t(xin) once (the reference recomputes it every iteration, deconv.py:104)
-    const float* bimg = xin;
-    if (d.kh > 0) {
-        ProfScope ps(3, s);
-        float* bb = at<float>(ws, Lo.b);
-        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(xin, spec[0], twW, rows, s); });
-        if (e) return e;
-        if ((e = pass_b(H, spec[0], fcT, mT, twH, N, (int)P, 1, s))) return e;
-        e = with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec[0], bb, twW, rows, s); });
-        if (e) return e;
-        bimg = bb;
-    }
-    {
-        ProfScope ps(3, s);
-        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, spec[0], twW, rows, s); });
-        if (e) return e;
-    }
-
-    int R = env_int("ADMM_PASSA_R", 0);
-    if (R <= 0) {
-        // rows per strip (measured on MI355X, tools/sweep.py): 8 for full-wave rows (W >= 1024),
-        // 16 below; halve while there are fewer than ~3 waves per SIMD of strips
-        const int L = std::min(64, N / (N >= 1024 ? 16 : N >= 64 ? 8 : N >= 16 ? 4 : 2));
-        const long long want = 3LL * 1024 * 64 / L;
-        R = N >= 512 ? 8 : 16;
-        while (R > 2 && rows / R < want) R /= 2;
-    }
-    if (R > H) R = H;
-
-    int cur = 0, uin = 0;  // spec[cur] holds the current r spectra; u[2*uin], u[2*uin+1] = u_x, u_y in
-    for (int it = 1; it <= d.maxit; ++it) {
+    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * BL.ntp * sizeof(float), s));
+    int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(gout, spec[0], twW, rows, s); });
+    if (e) return e;
+    int cur = 0, ain = 0;
+    for (int k = K; k >= 1; --k) {
         {
             ProfScope ps(1, s);
-            if (int e = pass_b(H, spec[cur], fcT, mT, twH, N, (int)P, 0, s)) return e;
+            if ((e = pass_b(H, spec[cur], fcT, mT, twH, N, (int)P, 0, s))) return e;
         }
-        if (it == d.maxit) {
-            ProfScope ps(3, s);
-            int e = with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec[cur], out, twW, rows, s); });
-            if (e) return e;
-            break;
-        }
-        const bool first = (it == 1);
-        float* uxi = u[2 * uin];
-        float* uyi = u[2 * uin + 1];
-        float* uxo = u[2 * (1 - uin)];
-        float* uyo = u[2 * (1 - uin) + 1];
-        const float* nsq = nullptr;
-        if (d.iso) {
+        const bool lastk = (k == K), firstk = (k == 1);
+        if (d.iso && !firstk) {
             ProfScope ps(2, s);
-            IsoArgs ia{spec[cur], uxi, uyi, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
-                       (long long)Lo.ngroups * H};
-            int e = with_row(N, [&](auto ops) { return decltype(ops)::iso_norm(ia, first, s); });
-            if (e) return e;
+            BwdIsoArgs qa{spec[cur], ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0), ha(k - 1, 1), rho,
+                          at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg, (long long)Lo.ngroups * H};
+            if ((e = with_row(N, [&](auto ops) { return decltype(ops)::bwd_iso_q(qa, lastk, s); }))) return e;
             const long long n4 = 2LL * H * W / 4;
             hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                               at<float4>(ws, Lo.part), at<float4>(ws, Lo.nsq), Lo.ngroups, n4);
+                               at<float4>(ws, Lo.part), reinterpret_cast<float4*>(q), Lo.ngroups, n4);
             if ((e = launch_check("k_iso_reduce"))) return e;
-            nsq = at<float>(ws, Lo.nsq);
+            hipLaunchKernelGGL(k_iso_tau_partial, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
+                               tpart + (size_t)(K - k) * BL.ntp, 2LL * H * W);
+            if ((e = launch_check("k_iso_tau_partial"))) return e;
         }
         {
             ProfScope ps(0, s);
-            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, lam, rho, twW, H, R, rows / R};
-            int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, s); });
-            if (e) return e;
+            BwdArgs ba{spec[cur], spec[1 - cur], bbar,
+                       ab[2 * ain], ab[2 * ain + 1], ab[2 * (1 - ain)], ab[2 * (1 - ain) + 1],
+                       ha(k, 0), ha(k, 1),
+                       firstk ? nullptr : ha(k - 1, 0), firstk ? nullptr : ha(k - 1, 1),
+                       (d.iso && !firstk) ? hn(k - 1) : nullptr, q, lam, rho,
+                       part + (size_t)(K - k) * BL.nstrips * 2, twW, H, BL.R, BL.nstrips};
+            if ((e = with_row(N, [&](auto ops) { return decltype(ops)::bwd_pass_a(ba, d.iso != 0, lastk, firstk, s); })))
+                return e;
         }
         cur = 1 - cur;
-        uin = 1 - uin;
+        ain = 1 - ain;
+    }
+    if (glam && grho) {
+        hipLaunchKernelGGL(k_bwd_scalars, dim3(1), dim3(256), 0, s, part, (long long)K * BL.nstrips, tpart,
+                           d.iso ? K * BL.ntp : 0, lam, rho, glam, grho);
+        if ((e = launch_check("k_bwd_scalars"))) return e;
+    } else if (glam || grho) {
+        return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
+    }
+    if (gxin && d.kh > 0) {
+        // x^_in = H_t^T b^ : the conjugate multiplier (pass B mode 2)
+        if ((e = psf_transpose_into(d, Lo, ws, bbar, gxin, spec[0], 2, s))) return e;
     }
     return 0;
 }
@@ -413,13 +649,7 @@ int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float*
                        at<double2>(ws, Lo.twHd), at<float>(ws, Lo.fcT), at<float>(ws, Lo.spec[1]),
                        at<cf>(ws, Lo.mT), d.kh, H, N, W);
     if (int e = launch_check("k_spectra")) return e;
-    cf* twW = at<cf>(ws, Lo.twW);
-    const long long rows = P * H;
-    int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(xin, at<cf>(ws, Lo.spec[0]), twW, rows, s); });
-    if (e) return e;
-    if ((e = pass_b(H, at<cf>(ws, Lo.spec[0]), nullptr, at<cf>(ws, Lo.mT), at<cf>(ws, Lo.twH), N, (int)P, 1, s)))
-        return e;
-    return with_row(N, [&](auto ops) { return decltype(ops)::c2r(at<cf>(ws, Lo.spec[0]), out, twW, rows, s); });
+    return psf_transpose_into(d, Lo, ws, xin, out, at<cf>(ws, Lo.spec[0]), 1, s);
 }
 
 int admm_tv_profile_enable(int enable) {

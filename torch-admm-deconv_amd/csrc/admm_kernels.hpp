@@ -229,7 +229,8 @@ __global__ void __launch_bounds__(256) k_row_c2r(const cf* __restrict__ spec, fl
 
 // ---------------------------------------------------------------------------
 // pass B: column FFT -> multiply -> column IFFT, in place, C columns per block
-// MODE 0: real Wiener factor fcT;  MODE 1: complex multiplier mT (PSF transpose)
+// MODE 0: real Wiener factor fcT;  MODE 1: complex multiplier mT (PSF transpose H_t);
+// MODE 2: conj(mT) (the adjoint of H_t, for the input gradient)
 // ---------------------------------------------------------------------------
 // min waves per SIMD for pass B: as many blocks per CU as the LDS admits (<= 2)
 constexpr int pb_minw(int nt, size_t lds) {
@@ -283,7 +284,8 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
 #pragma unroll
         for (int j = 0; j < E; ++j) {
             if constexpr (MODE == 0) m[j] = bload_f(rm, mo, j * L * (int)sizeof(float));
-            else m[j] = bload_cf(rm, mo, j * L * (int)sizeof(cf));
+            else if constexpr (MODE == 1) m[j] = bload_cf(rm, mo, j * L * (int)sizeof(cf));
+            else m[j] = cconj(bload_cf(rm, mo, j * L * (int)sizeof(cf)));
         }
     }
     __syncthreads();
@@ -304,7 +306,7 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
                     const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
                     v[j] = mkc(fmaf(a, v[j].x, b * q.x), fmaf(a, v[j].y, b * q.y));
                 } else {
-                    const cf m0 = m[j], mn = mT[(size_t)N * H + ky];
+                    const cf m0 = m[j], mn = MODE == 1 ? mT[(size_t)N * H + ky] : cconj(mT[(size_t)N * H + ky]);
                     const cf a = mkc(0.5f * (m0.x + mn.x), 0.5f * (m0.y + mn.y));
                     const cf b = mkc(0.5f * (m0.x - mn.x), 0.5f * (m0.y - mn.y));
                     v[j] = cadd(cmul(v[j], a), cmul(q, b));
@@ -326,25 +328,53 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
 
 // ---------------------------------------------------------------------------
 // pass A: the fused row pass of one ADMM iteration, one sub-group per strip of R rows
+//
+// State between iterations (per plane, two images):
+//   inference  (HIST = false): u_{k-1} in, u_k out (ping-pong buffers)
+//   training   (HIST = true) : a_{k-1} in, a_k out, a_k = D x_k + u_{k-1} kept for every k
+//              (the backward needs it); u = a - S(a) and w = z - u are rebuilt in registers,
+//              so both modes move the same bytes.
 // ---------------------------------------------------------------------------
 struct PassAArgs {
-    const cf* sin;      // x row spectra (output of pass B)     [P][H][N]
-    cf* sout;           // r row spectra for the next pass B     [P][H][N]
-    const float* b;     // H_t(xin)                              [P][H][W]
-    const float* uxi;   // u_x, u_y of the previous iteration    [P][H][W]
+    const cf* sin;        // x row spectra (output of pass B)     [P][H][N]
+    cf* sout;             // r row spectra for the next pass B     [P][H][N]
+    const float* b;       // H_t(xin)                              [P][H][W]
+    const float* uxi;     // u_{k-1} (or a_{k-1} when HIST), x / y [P][H][W]
     const float* uyi;
-    float* uxo;         // u_x, u_y of this iteration (ping-pong)
+    float* uxo;           // u_k (or a_k when HIST)
     float* uyo;
-    const float* nsq;   // iso: per-pixel sum over (B,C) of a_x^2, a_y^2  [2][H][W]
+    const float* nsq;     // iso: N_k     = per-pixel sum over (B,C) of a_k^2      [2][H][W]
+    const float* nsq_prev;// iso + HIST: N_{k-1}
     const float* lam;
     const float* rho;
-    const cf* twW;      // [W]
+    const cf* twW;        // [W]
     int H;
-    int R;              // rows per strip (divides H)
+    int R;                // rows per strip (divides H)
     long long nstrips;
 };
 
-template <int N, bool ISO, bool FIRST>
+template <bool ISO> __device__ __forceinline__ float shrink_z(float a, float tau, float nsum) {
+    if constexpr (ISO) return block_factor(nsum, tau) * a;
+    else return soft(a, tau);
+}
+
+// u_{k-1} at a pixel pair: zero (first iteration), loaded, or rebuilt from a_{k-1}
+template <bool ISO, bool FIRST, bool HIST>
+__device__ __forceinline__ cf prev_u(const cf* __restrict__ src, const cf* __restrict__ nsp, size_t idx, float tau) {
+    if constexpr (FIRST) {
+        return mkc(0.f, 0.f);
+    } else {
+        const cf v = src[idx];
+        if constexpr (HIST) {
+            const cf n = ISO ? nsp[idx] : mkc(0.f, 0.f);
+            return mkc(v.x - shrink_z<ISO>(v.x, tau, n.x), v.y - shrink_z<ISO>(v.y, tau, n.y));
+        } else {
+            return v;
+        }
+    }
+}
+
+template <int N, bool ISO, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
     using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
@@ -373,6 +403,8 @@ __global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
     cf* uyo = reinterpret_cast<cf*>(a.uyo + poff);
     const cf* nsx = reinterpret_cast<const cf*>(a.nsq);
     const cf* nsy = reinterpret_cast<const cf*>(a.nsq + (size_t)H * W);
+    const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev);
+    const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + (size_t)H * W);
 
     cf xprev[E], xcur[E], wxp[E], wyp[E];
     {
@@ -388,29 +420,23 @@ __global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
         for (int j = 0; j < E; ++j) xcur[j] = sp[ro + t + L * j];
         RowXf<N>::c2r(xcur, buf, tw, t);
 
-        // ---- y direction: dy = x[g] - x[g-1]; z_y, u_y, w_y of row g
+        // ---- y direction: a_y = x[g] - x[g-1] + u_y; z_y, u_y, w_y of row g
         cf wyc[E];
         {
             cf uy[E], fy[E];
 #pragma unroll
             for (int j = 0; j < E; ++j) {
-                uy[j] = FIRST ? mkc(0.f, 0.f) : uyi[ro + t + L * j];
+                uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
                 if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
             }
 #pragma unroll
             for (int j = 0; j < E; ++j) {
                 const float a0 = (xcur[j].x - xprev[j].x) + uy[j].x;
                 const float a1 = (xcur[j].y - xprev[j].y) + uy[j].y;
-                float z0, z1;
-                if constexpr (ISO) {
-                    z0 = block_factor(fy[j].x, tau) * a0;
-                    z1 = block_factor(fy[j].y, tau) * a1;
-                } else {
-                    z0 = soft(a0, tau);
-                    z1 = soft(a1, tau);
-                }
+                const float z0 = shrink_z<ISO>(a0, tau, ISO ? fy[j].x : 0.f);
+                const float z1 = shrink_z<ISO>(a1, tau, ISO ? fy[j].y : 0.f);
                 const float n0 = a0 - z0, n1 = a1 - z1;  // u_y(new)
-                uy[j] = mkc(n0, n1);
+                uy[j] = HIST ? mkc(a0, a1) : mkc(n0, n1);
                 wyc[j] = mkc(z0 - n0, z1 - n1);
             }
             if (rr < R) {
@@ -439,12 +465,12 @@ __global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
             for (int j = 0; j < E; ++j) so[rm + t + L * j] = r[j];
         }
 
-        // ---- x direction: dx = x[g][j] - x[g][j-1]; z_x, u_x, w_x of row g
+        // ---- x direction: a_x = x[g][j] - x[g][j-1] + u_x; z_x, u_x, w_x of row g
         if (rr < R) {
             cf ux[E], fx[E], sh[E];
 #pragma unroll
             for (int j = 0; j < E; ++j) {
-                ux[j] = FIRST ? mkc(0.f, 0.f) : uxi[ro + t + L * j];
+                ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
                 if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
                 sh[j].x = __shfl(xcur[j].y, (t - 1) & (L - 1), L);
             }
@@ -453,16 +479,10 @@ __global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
                 const float xl = (t == 0) ? sh[(j - 1) & (E - 1)].x : sh[j].x;  // x at pixel q0-1
                 const float a0 = (xcur[j].x - xl) + ux[j].x;
                 const float a1 = (xcur[j].y - xcur[j].x) + ux[j].y;
-                float z0, z1;
-                if constexpr (ISO) {
-                    z0 = block_factor(fx[j].x, tau) * a0;
-                    z1 = block_factor(fx[j].y, tau) * a1;
-                } else {
-                    z0 = soft(a0, tau);
-                    z1 = soft(a1, tau);
-                }
+                const float z0 = shrink_z<ISO>(a0, tau, ISO ? fx[j].x : 0.f);
+                const float z1 = shrink_z<ISO>(a1, tau, ISO ? fx[j].y : 0.f);
                 const float n0 = a0 - z0, n1 = a1 - z1;
-                ux[j] = mkc(n0, n1);
+                ux[j] = HIST ? mkc(a0, a1) : mkc(n0, n1);
                 wxp[j] = mkc(z0 - n0, z1 - n1);
             }
 #pragma unroll
@@ -478,19 +498,22 @@ __global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
 
 // ---------------------------------------------------------------------------
 // iso pass A1: per-pixel partial sums over a group of planes of a_x^2, a_y^2
-// (a = D x + u), one sub-group per (plane group, row)
+// (a = D x + u_{k-1}), one sub-group per (plane group, row)
 // ---------------------------------------------------------------------------
 struct IsoArgs {
     const cf* sin;
-    const float* uxi;
+    const float* uxi;       // u_{k-1} (or a_{k-1} when HIST)
     const float* uyi;
+    const float* nsq_prev;  // HIST: N_{k-1}
+    const float* lam;
+    const float* rho;
     float* partial;  // [ngroups][2][H][W]
     const cf* twW;
     int P, H, ppg;   // planes per group
     long long nitems;  // ngroups * H
 };
 
-template <int N, bool FIRST>
+template <int N, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
     using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
@@ -506,6 +529,9 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
     const int grp = (int)(item / H);
     const int gm = (g - 1 + H) & (H - 1);
     RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    const float tau = HIST ? a.lam[0] / a.rho[0] : 0.f;
+    const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev);
+    const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + (size_t)H * W);
     cf sx[E], sy[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) sx[j] = sy[j] = mkc(0.f, 0.f);
@@ -521,6 +547,7 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
         RowXf<N>::c2r(xp, buf, tw, t);
         RowXf<N>::c2r(xc, buf, tw, t);
         const size_t ro = (size_t)p * H * N + (size_t)g * N;  // cf units == pixel pairs
+        const size_t rn = (size_t)g * N;                      // norm maps are per pixel, shared by planes
         const cf* uxi = reinterpret_cast<const cf*>(a.uxi);
         const cf* uyi = reinterpret_cast<const cf*>(a.uyi);
         cf sh[E];
@@ -528,8 +555,18 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
         for (int j = 0; j < E; ++j) sh[j].x = __shfl(xc[j].y, (t - 1) & (L - 1), L);
 #pragma unroll
         for (int j = 0; j < E; ++j) {
-            const cf ux = FIRST ? mkc(0.f, 0.f) : uxi[ro + t + L * j];
-            const cf uy = FIRST ? mkc(0.f, 0.f) : uyi[ro + t + L * j];
+            cf ux, uy;
+            if constexpr (FIRST) {
+                ux = uy = mkc(0.f, 0.f);
+            } else if constexpr (HIST) {
+                const cf ax = uxi[ro + t + L * j], ay = uyi[ro + t + L * j];
+                const cf nx = npx[rn + t + L * j], ny = npy[rn + t + L * j];
+                ux = mkc(ax.x - block_factor(nx.x, tau) * ax.x, ax.y - block_factor(nx.y, tau) * ax.y);
+                uy = mkc(ay.x - block_factor(ny.x, tau) * ay.x, ay.y - block_factor(ny.y, tau) * ay.y);
+            } else {
+                ux = uxi[ro + t + L * j];
+                uy = uyi[ro + t + L * j];
+            }
             const float xl = (t == 0) ? sh[(j - 1) & (E - 1)].x : sh[j].x;
             const float ax0 = (xc[j].x - xl) + ux.x, ax1 = (xc[j].y - xc[j].x) + ux.y;
             const float ay0 = (xc[j].x - xp[j].x) + uy.x, ay1 = (xc[j].y - xp[j].y) + uy.y;
