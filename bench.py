@@ -63,6 +63,27 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(config: str, kernel: str, launches: int, steps: int):
+    """Per-launch HBM traffic of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_summary.json, made by tools/pmc/run_pmc.sh + summarize.py: separate
+    FETCH_SIZE / WRITE_SIZE passes, gfx950 corrections calibrated on the box).  None if absent."""
+    import glob
+    if config != "c3":
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        summ = json.load(f)["kernels"]
+    if kernel == "pass_a":
+        first = summ.get("k_pass_a<512, false, true, false>", {}).get("traffic_bytes")
+        rest = summ.get("k_pass_a<512, false, false, false>", {}).get("traffic_bytes")
+        if first is None or rest is None or launches < steps:
+            return None, None
+        return (first * steps + rest * (launches - steps)) / launches, os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def cpu_baseline(cfg, planes, iters):
     """Oracle (reference op sequence: circular pad + depthwise conv operators, H_t
     recomputed every iteration, torch.fft x-update) on a bounded sample, on host cores."""
@@ -165,6 +186,7 @@ def main():
     dms, dn, dbytes = kern[dom]
     achieved = (dbytes / (dms / 1e3)) / 1e9 if dms > 0 else 0.0
 
+    traffic, traffic_src = pmc_traffic(args.config, dom, dn, K)
     result = None
     if rank == 0:
         parity = None
@@ -197,7 +219,8 @@ def main():
                        "maxit": maxit, "iso": iso, "parallelism": f"shard{world} (batch sharded, no data-path "
                                                                   "collective)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "traffic_source": traffic_src,
                          "launches": dn, "avg_launch_ms": dms / max(dn, 1),
                          "algorithmic_bytes_per_launch": dbytes / max(dn, 1),
                          "per_kernel": {n: {"ms_total": v[0], "launches": v[1],
