@@ -9,7 +9,8 @@ import ctypes
 import os
 import threading
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libadmm_tv.so")
+_LIB_PATH = os.environ.get("ADMMTOR_LIB_OVERRIDE") or \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libadmm_tv.so")  # override: tuning A/B only
 
 ADMM_TV_OK = 0
 ADMM_TV_EINVAL = -1

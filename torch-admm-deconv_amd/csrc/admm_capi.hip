@@ -315,11 +315,12 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
 int strip_rows(int H, int N, long long rows) {
     int R = env_int("ADMM_PASSA_R", 0);
     if (R <= 0) {
-        // rows per strip (measured on MI355X, tools/sweep.py): 8 for full-wave rows (W >= 1024),
-        // 16 below; halve while there are fewer than ~3 waves per SIMD of strips
+        // rows per strip (measured on MI355X, tools/sweep.py: R = 8 beats 16 at W = 512 and
+        // 1024 with the 3-waves/SIMD row pass); halve while there are fewer than ~3 waves per
+        // SIMD of strips
         const int L = std::min(64, N / (N >= 1024 ? 16 : N >= 64 ? 8 : N >= 16 ? 4 : 2));
         const long long want = 3LL * 1024 * 64 / L;
-        R = N >= 512 ? 8 : 16;
+        R = 8;
         while (R > 2 && rows / R < want) R /= 2;
     }
     if (R > H) R = H;

@@ -353,6 +353,13 @@ struct PassAArgs {
     long long nstrips;
 };
 
+// occupancy target of the row pass (waves per SIMD): 3 for rows up to W = 1024 (fits
+// ~168 VGPRs, measured faster than 2), 1 for W = 2048 (E = 16 per lane)
+#ifndef PASSA_MINW_SMALL
+#define PASSA_MINW_SMALL 3
+#endif
+#define PASSA_MINW(n) ((n) >= 1024 ? 1 : PASSA_MINW_SMALL)
+
 template <bool ISO> __device__ __forceinline__ float shrink_z(float a, float tau, float nsum) {
     if constexpr (ISO) return block_factor(nsum, tau) * a;
     else return soft(a, tau);
@@ -375,7 +382,7 @@ __device__ __forceinline__ cf prev_u(const cf* __restrict__ src, const cf* __res
 }
 
 template <int N, bool ISO, bool FIRST, bool HIST>
-__global__ void __launch_bounds__(256) k_pass_a(PassAArgs a) {
+__global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
     using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
