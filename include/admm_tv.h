@@ -101,6 +101,16 @@ int admm_tv_backward(const admm_tv_desc* desc, const float* kern, const float* l
 int admm_tv_psf_transpose(const admm_tv_desc* desc, const float* xin, const float* kern,
                           float* out, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Cross-rank reduction hook for iso (block) shrinkage over a batch sharded across
+ * GPUs.  The per-pixel norm couples every (b,c) plane, so each
+ * iteration the library calls fn(buf, count, stream, ctx) on its per-pixel sums
+ * (count = 2*H*W floats, device memory inside the workspace or history buffer)
+ * and expects an in-place SUM all-reduce ordered on `stream` (e.g. RCCL).  In the
+ * backward the same is called on the cross-plane products Q.  NULL disables
+ * (single process).  Global to the process; not used for iso = 0.               */
+typedef void (*admm_tv_allreduce_fn)(float* buf, size_t count, void* stream, void* ctx);
+int admm_tv_set_allreduce(admm_tv_allreduce_fn fn, void* ctx);
+
 /* Per-kernel timing of the iteration passes (HIP events on the launch stream),
  * used by bench.py for the roofline line.  enable != 0 starts recording;
  * read() synchronises on the recorded events and returns totals since the last

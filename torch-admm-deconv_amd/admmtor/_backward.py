@@ -14,6 +14,8 @@ implemented yet: requesting it raises.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 from . import _native
@@ -32,7 +34,7 @@ class AdmmTvFunction(torch.autograd.Function):
     """out = fft_admm_tv(xin, lam, rho, kern, iso, maxit) with a native backward."""
 
     @staticmethod
-    def forward(ctx, x32, lam, rho, k32, iso: bool, maxit: int):
+    def forward(ctx, x32, lam, rho, k32, iso: bool, maxit: int, hook=None):
         lib = _native.load()
         B, C, H, W = x32.shape
         k = int(k32.shape[-1]) if k32.numel() > 0 else 0
@@ -44,10 +46,14 @@ class AdmmTvFunction(torch.autograd.Function):
         hist = torch.empty(max(_native.history_size(d), 1), dtype=torch.uint8, device=x32.device)
         out = torch.empty_like(x32)
         stream = torch.cuda.current_stream(x32.device).cuda_stream
-        _native.check(lib.admm_tv_forward_train(
-            d, x32.data_ptr(), k32c.data_ptr() if k > 0 else None, lam_c.data_ptr(), rho_c.data_ptr(),
-            out.data_ptr(), hist.data_ptr(), hist.numel(), ws.data_ptr(), ws.numel(), stream))
+        hook = hook if iso else None
+        with (hook if hook is not None else contextlib.nullcontext()):
+            _native.register_buffers(ws, hist)
+            _native.check(lib.admm_tv_forward_train(
+                d, x32.data_ptr(), k32c.data_ptr() if k > 0 else None, lam_c.data_ptr(), rho_c.data_ptr(),
+                out.data_ptr(), hist.data_ptr(), hist.numel(), ws.data_ptr(), ws.numel(), stream))
         del ws
+        ctx.hook = hook
         ctx.save_for_backward(k32c, lam_c, rho_c)
         ctx.hist = hist
         ctx.desc = (B, C, H, W, k, iso, maxit)
@@ -71,26 +77,28 @@ class AdmmTvFunction(torch.autograd.Function):
         gr = torch.empty(1, dtype=torch.float32, device=dev) if need_s else None
         ws = torch.empty(_native.backward_workspace_size(d), dtype=torch.uint8, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
-        _native.check(lib.admm_tv_backward(
-            d, k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(), g.data_ptr(),
-            ctx.hist.data_ptr(), ctx.hist.numel(),
-            gx.data_ptr() if gx is not None else None,
-            gl.data_ptr() if gl is not None else None,
-            gr.data_ptr() if gr is not None else None,
-            ws.data_ptr(), ws.numel(), stream))
+        with (ctx.hook if ctx.hook is not None else contextlib.nullcontext()):
+            _native.register_buffers(ws, ctx.hist)
+            _native.check(lib.admm_tv_backward(
+                d, k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(), g.data_ptr(),
+                ctx.hist.data_ptr(), ctx.hist.numel(),
+                gx.data_ptr() if gx is not None else None,
+                gl.data_ptr() if gl is not None else None,
+                gr.data_ptr() if gr is not None else None,
+                ws.data_ptr(), ws.numel(), stream))
         ctx.hist = None  # release the history as soon as the gradient is formed
         return (gx,
                 gl if ctx.needs_input_grad[1] else None,
                 gr if ctx.needs_input_grad[2] else None,
-                None, None, None)
+                None, None, None, None)
 
 
-def fft_admm_tv_autograd(xin, lmbd, rho, kern, iso, maxit):
+def fft_admm_tv_autograd(xin, lmbd, rho, kern, iso, maxit, hook=None):
     dev = xin.device
     x32 = xin.to(torch.float32)  # differentiable cast (autocast / half inputs)
     k32 = kern.to(device=dev, dtype=torch.float32) if kern.numel() > 0 else \
         torch.empty(0, dtype=torch.float32, device=dev)
     lam_t, _ = _scalar_input(lmbd, dev)
     rho_t, _ = _scalar_input(rho, dev)
-    out = AdmmTvFunction.apply(x32, lam_t, rho_t, k32, bool(iso), int(maxit))
+    out = AdmmTvFunction.apply(x32, lam_t, rho_t, k32, bool(iso), int(maxit), hook)
     return out

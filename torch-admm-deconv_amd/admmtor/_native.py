@@ -31,6 +31,7 @@ EXPORTED = (
     "admm_tv_forward_train",
     "admm_tv_backward_workspace_size",
     "admm_tv_backward",
+    "admm_tv_set_allreduce",
     "admm_tv_profile_enable",
     "admm_tv_profile_reset",
     "admm_tv_profile_read",
@@ -49,6 +50,9 @@ class AdmmTvDesc(ctypes.Structure):
         ("iso", ctypes.c_int32),
         ("maxit", ctypes.c_int32),
     ]
+
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
 
 
 class NativeError(RuntimeError):
@@ -99,6 +103,8 @@ def load() -> ctypes.CDLL:
         L.admm_tv_backward.argtypes = [dp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, sz, vp]
         L.admm_tv_psf_transpose.restype = ctypes.c_int
         L.admm_tv_psf_transpose.argtypes = [dp, vp, vp, vp, vp, sz, vp]
+        L.admm_tv_set_allreduce.restype = ctypes.c_int
+        L.admm_tv_set_allreduce.argtypes = [ALLREDUCE_FN, vp]
         L.admm_tv_profile_enable.restype = ctypes.c_int
         L.admm_tv_profile_enable.argtypes = [ctypes.c_int]
         L.admm_tv_profile_reset.restype = ctypes.c_int
@@ -143,6 +149,51 @@ def backward_workspace_size(d: AdmmTvDesc) -> int:
 
 def supported(H: int, W: int) -> bool:
     return bool(load().admm_tv_supported(int(H), int(W)))
+
+
+# --------------------------------------------------------------------------- cross-rank hook
+# Device buffers the library may hand to the all-reduce callback live inside tensors the
+# Python side allocated (workspace, history); the callback maps the raw pointer back to a
+# view of one of them.
+_live_buffers = []
+
+
+def register_buffers(*tensors):
+    _live_buffers[:] = [t for t in tensors if t is not None]
+
+
+def _view_of(ptr: int, count: int):
+    import torch
+    nbytes = 4 * count
+    for t in _live_buffers:
+        base = t.data_ptr()
+        if base <= ptr and ptr + nbytes <= base + t.numel() * t.element_size():
+            off = ptr - base
+            return t.view(torch.uint8)[off:off + nbytes].view(torch.float32)
+    raise RuntimeError("admmtor: all-reduce buffer not inside a registered workspace")
+
+
+class AllReduceHook:
+    """Context manager installing a SUM all-reduce (torch.distributed) for iso sharding."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self._dist = dist
+        self._group = group
+        self._cb = ALLREDUCE_FN(self._call)
+
+    def _call(self, ptr, count, stream, ctx):
+        t = _view_of(int(ptr), int(count))
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self._group)
+
+    def __enter__(self):
+        check(load().admm_tv_set_allreduce(self._cb, None))
+        return self
+
+    def __exit__(self, *exc):
+        check(load().admm_tv_set_allreduce(ALLREDUCE_FN(), None))
+        register_buffers()
+        return False
 
 
 def profile_enable(on: bool) -> None:

@@ -15,6 +15,7 @@ Drop-in for ``/root/reference/src/admmtor/eops/deconv.py``:
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Tuple
 
 import torch
@@ -107,8 +108,10 @@ def _as_device_scalar(v, device) -> torch.Tensor:
     return torch.full((1,), float(v), dtype=torch.float32, device=device)
 
 
-def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.Tensor, iso: bool, maxit: int):
-    """Run the HIP solver: x32 (B,C,H,W) fp32 contiguous on the device -> new tensor."""
+def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.Tensor, iso: bool, maxit: int,
+           hook=None):
+    """Run the HIP solver: x32 (B,C,H,W) fp32 contiguous on the device -> new tensor.
+    `hook`: an _native.AllReduceHook for iso over a batch sharded across ranks."""
     lib = _native.load()
     B, C, H, W = x32.shape
     k = int(k32.shape[-1]) if k32.numel() > 0 else 0
@@ -120,9 +123,11 @@ def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.T
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
     out = torch.empty_like(x32)
     stream = torch.cuda.current_stream(x32.device).cuda_stream
-    _native.check(lib.admm_tv_forward(
-        d, x32.data_ptr(), k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(),
-        out.data_ptr(), ws.data_ptr(), ws.numel(), stream))
+    with (hook if (hook is not None and iso) else contextlib.nullcontext()):
+        _native.register_buffers(ws)
+        _native.check(lib.admm_tv_forward(
+            d, x32.data_ptr(), k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(),
+            out.data_ptr(), ws.data_ptr(), ws.numel(), stream))
     return out
 
 
@@ -141,6 +146,11 @@ def fft_admm_tv(xin: torch.Tensor,
     last x with xin's shape.  Runs on ROCm tensors only (fp32; bf16/fp16 under
     ``torch.autocast`` compute in fp32 and return fp32, as the reference does).
     """
+    return _fft_admm_tv_impl(xin, lmbd, rho, kern, iso, maxit)
+
+
+def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> torch.Tensor:
+    """fft_admm_tv with an optional cross-rank all-reduce hook (admmtor.sharded)."""
     if not isinstance(kern, torch.Tensor):
         kern = torch.as_tensor(kern)
     _check_inputs(xin, kern)
@@ -159,5 +169,5 @@ def fft_admm_tv(xin: torch.Tensor,
         or (isinstance(rho, torch.Tensor) and rho.requires_grad) or kern.requires_grad)
     if needs_grad:
         from .._backward import fft_admm_tv_autograd
-        return fft_admm_tv_autograd(xin, lmbd, rho, kern, bool(iso), maxit)
-    return _solve(x32, k32, lam, rh, bool(iso), maxit)
+        return fft_admm_tv_autograd(xin, lmbd, rho, kern, bool(iso), maxit, hook=hook)
+    return _solve(x32, k32, lam, rh, bool(iso), maxit, hook=hook)

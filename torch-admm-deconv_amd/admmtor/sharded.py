@@ -5,8 +5,9 @@ independent problem, so a batch is split across ranks with NO per-iteration
 communication.  The only collectives are a broadcast of the PSF, lambda and rho
 from rank 0 (a few KB: every rank then builds its own Wiener factor) and,
 optionally, a final gather of the outputs.  iso=True couples the whole batch
-through the per-pixel (B, C) norm and needs a per-iteration all-reduce; that
-mode is not sharded yet (raises for world > 1).
+through the per-pixel (B, C) norm: it is sharded with a per-iteration SUM
+all-reduce of the 2*H*W per-pixel sums (RCCL), installed through the C ABI hook
+``admm_tv_set_allreduce`` (and of the cross-plane products Q in the backward).
 
 The reference has no distributed code at all; this module is the
 multi-GPU layer of the MI355X build.
@@ -35,22 +36,36 @@ def _as_tensor(v, device, dtype=torch.float32):
 
 
 def broadcast_params(kern: torch.Tensor, lmbd, rho, group=None, src: int = 0, device=None):
-    """Broadcast (kern, lambda, rho) from `src` to every rank of `group`.
+    """Broadcast (kern, lambda, rho) from `src` to every rank of `group` (one packed collective).
 
     Non-source ranks only need to pass a kern of the right size (its values are
-    overwritten).  Returns device tensors: kern (1,1,k,k) or empty, lambda (1,), rho (1,).
+    overwritten).  Tensors that require grad are trainable parameters replicated by
+    the training framework (DDP keeps them identical): they are returned unchanged so
+    autograd reaches them.  Returns kern (1,1,k,k) or empty, lambda (1,), rho (1,).
     """
     device = device or (kern.device if kern.numel() else torch.device("cpu"))
-    k = kern.detach().to(device=device, dtype=torch.float32).contiguous().clone() if kern.numel() else \
-        torch.empty(0, device=device)
-    lam = _as_tensor(lmbd, device)
-    rh = _as_tensor(rho, device)
+
+    def trainable(v):
+        return isinstance(v, torch.Tensor) and v.requires_grad
+
+    k = kern if trainable(kern) else (kern.detach().to(device=device, dtype=torch.float32).contiguous().clone()
+                                      if kern.numel() else torch.empty(0, device=device))
+    lam = lmbd if trainable(lmbd) else _as_tensor(lmbd, device)
+    rh = rho if trainable(rho) else _as_tensor(rho, device)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        packed = torch.cat([lam, rh, k.reshape(-1)])  # one collective for all three
-        dist.broadcast(packed, src=src, group=group)
-        lam, rh = packed[0:1], packed[1:2]
-        if k.numel():
-            k = packed[2:].reshape(k.shape)
+        parts = [t for t in (lam, rh, k) if not trainable(t)]
+        if parts:
+            packed = torch.cat([t.reshape(-1) for t in parts])
+            dist.broadcast(packed, src=src, group=group)
+            off = 0
+            out = []
+            for t in (lam, rh, k):
+                if trainable(t):
+                    out.append(t)
+                else:
+                    out.append(packed[off:off + t.numel()].reshape(t.shape))
+                    off += t.numel()
+            lam, rh, k = out
     return k, lam, rh
 
 
@@ -65,12 +80,14 @@ def sharded_fft_admm_tv(x_local: torch.Tensor, lmbd, rho, kern: torch.Tensor, is
                  to equal size internally)
     solver       defaults to admmtor.eops.deconv.fft_admm_tv (the HIP path)
     """
-    if solver is None:
-        from admmtor.eops.deconv import fft_admm_tv as solver
     world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
-    if world > 1 and iso:
-        raise NotImplementedError("iso=True couples the whole batch (per-pixel norm over B and C): "
-                                  "batch sharding needs a per-iteration all-reduce, not implemented yet")
+    if solver is None:
+        from admmtor import _native
+        from admmtor.eops.deconv import _fft_admm_tv_impl
+        hook = _native.AllReduceHook(group) if (iso and world > 1) else None
+
+        def solver(x, l, r, k, i, m):
+            return _fft_admm_tv_impl(x, l, r, k, i, m, hook=hook)
     k, lam, rh = broadcast_params(kern, lmbd, rho, group=group, device=x_local.device)
     out = solver(x_local, lam, rh, k, iso, maxit)
     if gather is None or world == 1:

@@ -70,6 +70,13 @@ struct ProfScope {
     }
 };
 
+// ------------------------------------------------------------------ cross-rank reduction hook (iso)
+typedef void (*allreduce_fn)(float* buf, size_t count, void* stream, void* ctx);
+struct AllReduce {
+    allreduce_fn fn = nullptr;
+    void* ctx = nullptr;
+} g_allreduce;
+
 // ------------------------------------------------------------------ geometry
 bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 
@@ -443,6 +450,8 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
             hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
                                at<float4>(ws, Lo.part), reinterpret_cast<float4*>(nout), Lo.ngroups, n4);
             if ((e = launch_check("k_iso_reduce"))) return e;
+            // sharded batch: the per-pixel sums must cover every rank's planes
+            if (g_allreduce.fn) g_allreduce.fn(nout, 2ull * H * W, s, g_allreduce.ctx);
             nsq = nout;
         }
         {
@@ -597,9 +606,12 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* kern, const float* lam
             hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
                                at<float4>(ws, Lo.part), reinterpret_cast<float4*>(q), Lo.ngroups, n4);
             if ((e = launch_check("k_iso_reduce"))) return e;
+            // tau^ partial from this rank's Q (the norm N is already global): summing the
+            // ranks' lambda/rho gradients then counts every plane once
             hipLaunchKernelGGL(k_iso_tau_partial, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
                                tpart + (size_t)(K - k) * BL.ntp, 2LL * H * W);
             if ((e = launch_check("k_iso_tau_partial"))) return e;
+            if (g_allreduce.fn) g_allreduce.fn(q, 2ull * H * W, s, g_allreduce.ctx);
         }
         {
             ProfScope ps(0, s);
@@ -651,6 +663,12 @@ int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float*
                        at<cf>(ws, Lo.mT), d.kh, H, N, W);
     if (int e = launch_check("k_spectra")) return e;
     return psf_transpose_into(d, Lo, ws, xin, out, at<cf>(ws, Lo.spec[0]), 1, s);
+}
+
+int admm_tv_set_allreduce(admm_tv_allreduce_fn fn, void* ctx) {
+    g_allreduce.fn = fn;
+    g_allreduce.ctx = ctx;
+    return 0;
 }
 
 int admm_tv_profile_enable(int enable) {
