@@ -207,8 +207,16 @@ for i, c in enumerate(cases):
                 "values": {k: v.flatten().tolist() for k, v in sd.items()},
                 "shapes": {k: list(v.shape) for k, v in sd.items()}})
 print(json.dumps(out))
+# a reference-format checkpoint (saver.py:49-54 layout) of a trained-looking module
+torch.manual_seed(7)
+m = ADMMDeconv((5, 5), max_iters=7, iso=False, bias=True)
+with torch.no_grad():
+    m.lmbda.fill_(0.031); m.rho.fill_(0.047); m.b.fill_(0.25)
+torch.save({"epoch": 3, "model_state_dict": m.state_dict(), "optimizer_state_dict": {}, "loss": 0.5},
+           OUT_CKPT)
 """
     env = dict(os.environ, PYTHONPATH="/root/reference/src", PYTHONDONTWRITEBYTECODE="1")
+    code = code.replace("OUT_CKPT", repr(os.path.join(OUT, "ref_admmdeconv_ckpt.tar")))
     res = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True, cwd="/tmp")
     with open(os.path.join(OUT, "module_init.json"), "w") as f:
         f.write(res.stdout)

@@ -86,3 +86,34 @@ def test_admmdeconv_loads_reference_style_checkpoint():
     dst.load_state_dict(src.state_dict())
     for k in ("w", "lmbda", "rho", "b"):
         assert torch.equal(getattr(src, k), getattr(dst, k))
+
+
+def test_reference_checkpoint_loads():
+    """a checkpoint written by the reference's ADMMDeconv (saver.py:49-54 layout) loads into this
+    build's module with the safe loader (weights_only=True), values intact."""
+    from admmtor.elayers.admmdeconv import ADMMDeconv
+    ck = torch.load(os.path.join(GOLDEN, "ref_admmdeconv_ckpt.tar"), weights_only=True, map_location="cpu")
+    m = ADMMDeconv((5, 5), max_iters=7, iso=False, bias=True)
+    m.load_state_dict(ck["model_state_dict"])
+    assert m.lmbda.item() == pytest.approx(0.031) and m.rho.item() == pytest.approx(0.047)
+    assert m.b.item() == pytest.approx(0.25) and m.w.shape == (1, 1, 5, 5)
+    assert torch.equal(m.w.detach(), ck["model_state_dict"]["w"])
+
+
+def test_clamp_regularisers():
+    from admmtor.elayers.admmdeconv import ADMMDeconv
+    from admmtor.modelbuild.eregularizers import ADMMClipper, ADMMWeightClipper, WeightClipper
+    m = torch.nn.Sequential(ADMMDeconv((3, 3), 5), ADMMDeconv((), 5))
+    with torch.no_grad():
+        m[0].lmbda.fill_(-1.0)
+        m[0].rho.fill_(9.0)
+        m[0].w.fill_(3.0)
+        m[1].lmbda.fill_(0.0)
+    m.apply(ADMMClipper(2.0))
+    assert m[0].lmbda.item() == pytest.approx(1e-9) and m[0].rho.item() == 2.0 and m[1].lmbda.item() == 1e-9
+    m.apply(ADMMWeightClipper((-0.5, 0.5)))
+    assert m[0].w.max().item() == 0.5
+    with torch.no_grad():
+        m[0].rho.fill_(9.0)
+    m.apply(WeightClipper())
+    assert m[0].rho.item() == 5.0
