@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ADMM_TV_ABI_VERSION 1
+#define ADMM_TV_ABI_VERSION 2
 
 enum {
     ADMM_TV_OK = 0,
@@ -53,7 +53,12 @@ typedef struct admm_tv_desc {
     int32_t kh, kw;
     int32_t iso;
     int32_t maxit;
+    int32_t flags;   /* ADMM_TV_FLAG_*; 0 for plain use */
 } admm_tv_desc;
+
+/* flags: the training forward also keeps the spectra of every r_k so that
+ * admm_tv_backward can form the PSF gradient (history grows by 4 B/pixel/iteration). */
+#define ADMM_TV_FLAG_PSF_GRAD 1
 
 /* ABI version (ADMM_TV_ABI_VERSION). */
 int admm_tv_abi_version(void);
@@ -89,11 +94,13 @@ int admm_tv_forward_train(const admm_tv_desc* desc, const float* xin, const floa
 
 /* Backward: given gout = dL/dx_K and the training history, writes dL/dxin
  * (gxin, may be NULL), dL/dlambda and dL/drho (glam, grho: device scalars, both or
- * neither).  The PSF gradient is not produced by this version.                  */
+ * neither) and, when desc->flags has ADMM_TV_FLAG_PSF_GRAD (also at the forward),
+ * dL/dkern (gkern, kh*kw floats; xin must then be given).                         */
 int admm_tv_backward_workspace_size(const admm_tv_desc* desc, size_t* bytes);
-int admm_tv_backward(const admm_tv_desc* desc, const float* kern, const float* lambda_dev,
-                     const float* rho_dev, const float* gout, const void* hist, size_t hist_bytes,
-                     float* gxin, float* glam, float* grho,
+int admm_tv_backward(const admm_tv_desc* desc, const float* xin, const float* kern,
+                     const float* lambda_dev, const float* rho_dev, const float* gout,
+                     const void* hist, size_t hist_bytes,
+                     float* gxin, float* glam, float* grho, float* gkern,
                      void* workspace, size_t workspace_bytes, void* stream);
 
 /* b = H_t(xin): the reference's circular PSF "adjoint" (a centred circular

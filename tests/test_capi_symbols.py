@@ -49,7 +49,7 @@ def test_library_is_gfx950_code():
 def test_host_entry_points():
     from admmtor import _native
     lib = _native.load()
-    assert lib.admm_tv_abi_version() == 1
+    assert lib.admm_tv_abi_version() == 2
     assert _native.supported(1024, 1024) and _native.supported(16, 2048) and _native.supported(4096, 16)
     assert not _native.supported(15, 17) and not _native.supported(1024, 4096) and not _native.supported(8, 64)
     d = _native.desc(64, 3, 1024, 1024, 21, False, 50)

@@ -9,8 +9,10 @@ the iteration in reverse with the same two-pass structure: r^_k = M x^_k in the
 column pass, then one fused row pass for the stencils and shrink Jacobians.
 
 Gradients: xin (through H_t and every iteration), lambda and rho (scalars; rho also
-through the Wiener factor, using dM/drho = -M D^T D M).  The PSF gradient is not
-implemented yet: requesting it raises.
+through the Wiener factor, using dM/drho = -M D^T D M) and the PSF (through b = H_t(xin)
+and through |sigma|^2 in the Wiener factor: a per-frequency cross-spectrum accumulated over
+planes and iterations, csrc/admm_backward.hpp).  The PSF path keeps each iteration's r_k
+spectrum (4 B/pixel/iteration more history) and is only enabled when the PSF requires grad.
 """
 from __future__ import annotations
 
@@ -34,11 +36,12 @@ class AdmmTvFunction(torch.autograd.Function):
     """out = fft_admm_tv(xin, lam, rho, kern, iso, maxit) with a native backward."""
 
     @staticmethod
-    def forward(ctx, x32, lam, rho, k32, iso: bool, maxit: int, hook=None):
+    def forward(ctx, x32, lam, rho, k32, iso: bool, maxit: int, hook=None, psf_grad: bool = False):
         lib = _native.load()
         B, C, H, W = x32.shape
         k = int(k32.shape[-1]) if k32.numel() > 0 else 0
-        d = _native.desc(B, C, H, W, k, iso, maxit)
+        flags = _native.ADMM_TV_FLAG_PSF_GRAD if (psf_grad and k > 0) else 0
+        d = _native.desc(B, C, H, W, k, iso, maxit, flags)
         x32 = x32.contiguous()
         k32c = k32.contiguous()
         lam_c, rho_c = lam.contiguous(), rho.contiguous()
@@ -54,19 +57,19 @@ class AdmmTvFunction(torch.autograd.Function):
                 out.data_ptr(), hist.data_ptr(), hist.numel(), ws.data_ptr(), ws.numel(), stream))
         del ws
         ctx.hook = hook
-        ctx.save_for_backward(k32c, lam_c, rho_c)
+        ctx.save_for_backward(k32c, lam_c, rho_c, x32 if flags else None)
         ctx.hist = hist
-        ctx.desc = (B, C, H, W, k, iso, maxit)
+        ctx.desc = (B, C, H, W, k, iso, maxit, flags)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        if ctx.needs_input_grad[3]:
-            raise NotImplementedError("admmtor (MI355X build): the gradient w.r.t. the PSF (kern / ADMMDeconv.w) "
-                                      "is not implemented yet; freeze the PSF (requires_grad_(False))")
-        k32, lam, rho = ctx.saved_tensors
-        B, C, H, W, k, iso, maxit = ctx.desc
-        d = _native.desc(B, C, H, W, k, iso, maxit)
+        k32, lam, rho, x32 = ctx.saved_tensors
+        B, C, H, W, k, iso, maxit, flags = ctx.desc
+        d = _native.desc(B, C, H, W, k, iso, maxit, flags)
+        need_k = ctx.needs_input_grad[3] and k > 0
+        if need_k and not flags:
+            raise RuntimeError("admmtor: PSF gradient requested but the forward did not keep the spectra")
         lib = _native.load()
         dev = gout.device
         g = gout.contiguous().to(torch.float32)
@@ -75,22 +78,24 @@ class AdmmTvFunction(torch.autograd.Function):
         gx = torch.empty((B, C, H, W), dtype=torch.float32, device=dev) if need_x else None
         gl = torch.empty(1, dtype=torch.float32, device=dev) if need_s else None
         gr = torch.empty(1, dtype=torch.float32, device=dev) if need_s else None
+        gk = torch.empty((1, 1, k, k), dtype=torch.float32, device=dev) if need_k else None
         ws = torch.empty(_native.backward_workspace_size(d), dtype=torch.uint8, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
         with (ctx.hook if ctx.hook is not None else contextlib.nullcontext()):
             _native.register_buffers(ws, ctx.hist)
             _native.check(lib.admm_tv_backward(
-                d, k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(), g.data_ptr(),
-                ctx.hist.data_ptr(), ctx.hist.numel(),
+                d, x32.data_ptr() if x32 is not None else None, k32.data_ptr() if k > 0 else None,
+                lam.data_ptr(), rho.data_ptr(), g.data_ptr(), ctx.hist.data_ptr(), ctx.hist.numel(),
                 gx.data_ptr() if gx is not None else None,
                 gl.data_ptr() if gl is not None else None,
                 gr.data_ptr() if gr is not None else None,
+                gk.data_ptr() if gk is not None else None,
                 ws.data_ptr(), ws.numel(), stream))
         ctx.hist = None  # release the history as soon as the gradient is formed
         return (gx,
                 gl if ctx.needs_input_grad[1] else None,
                 gr if ctx.needs_input_grad[2] else None,
-                None, None, None, None)
+                gk, None, None, None, None)
 
 
 def fft_admm_tv_autograd(xin, lmbd, rho, kern, iso, maxit, hook=None):
@@ -100,5 +105,6 @@ def fft_admm_tv_autograd(xin, lmbd, rho, kern, iso, maxit, hook=None):
         torch.empty(0, dtype=torch.float32, device=dev)
     lam_t, _ = _scalar_input(lmbd, dev)
     rho_t, _ = _scalar_input(rho, dev)
-    out = AdmmTvFunction.apply(x32, lam_t, rho_t, k32, bool(iso), int(maxit), hook)
+    psf_grad = isinstance(kern, torch.Tensor) and kern.requires_grad and kern.numel() > 0
+    out = AdmmTvFunction.apply(x32, lam_t, rho_t, k32, bool(iso), int(maxit), hook, psf_grad)
     return out

@@ -49,7 +49,12 @@ class AdmmTvDesc(ctypes.Structure):
         ("kw", ctypes.c_int32),
         ("iso", ctypes.c_int32),
         ("maxit", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
     ]
+
+
+ADMM_TV_FLAG_PSF_GRAD = 1
+ABI_VERSION = 2
 
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
@@ -100,7 +105,7 @@ def load() -> ctypes.CDLL:
         L.admm_tv_backward_workspace_size.restype = ctypes.c_int
         L.admm_tv_backward_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
         L.admm_tv_backward.restype = ctypes.c_int
-        L.admm_tv_backward.argtypes = [dp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, sz, vp]
+        L.admm_tv_backward.argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, sz, vp]
         L.admm_tv_psf_transpose.restype = ctypes.c_int
         L.admm_tv_psf_transpose.argtypes = [dp, vp, vp, vp, vp, sz, vp]
         L.admm_tv_set_allreduce.restype = ctypes.c_int
@@ -113,7 +118,7 @@ def load() -> ctypes.CDLL:
         L.admm_tv_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
         L.admm_tv_last_error.restype = ctypes.c_char_p
         L.admm_tv_last_error.argtypes = []
-        if L.admm_tv_abi_version() != 1:
+        if L.admm_tv_abi_version() != ABI_VERSION:
             raise ImportError("admmtor: native library ABI version mismatch")
         _lib = L
         return L
@@ -125,8 +130,8 @@ def check(code: int) -> None:
         raise NativeError(code, msg)
 
 
-def desc(B, C, H, W, k, iso, maxit) -> AdmmTvDesc:
-    return AdmmTvDesc(int(B), int(C), int(H), int(W), int(k), int(k), int(bool(iso)), int(maxit))
+def desc(B, C, H, W, k, iso, maxit, flags=0) -> AdmmTvDesc:
+    return AdmmTvDesc(int(B), int(C), int(H), int(W), int(k), int(k), int(bool(iso)), int(maxit), int(flags))
 
 
 def workspace_size(d: AdmmTvDesc) -> int:

@@ -397,3 +397,163 @@ __global__ void k_accum_parts(const float* __restrict__ part, long long n, float
 }
 
 }  // namespace admm
+
+namespace admm {
+
+// ---------------------------------------------------------------------------
+// PSF gradient.  The PSF k enters through b = H_t(xin) (centred circular
+// convolution, anchor c) and through s2 = |sigma|^2 in the Wiener factor.  With G = K^T K
+// (spectrum s2), dM = -M dG M, so dL = -sum_k <r^_k, dG x_k>; in Fourier (half plane,
+// c(kx) = 2 for 0 < kx < N else 1):
+//   dL/ds2(f)  = -(1/HW) c(kx) sum_k sum_p fc(f)^2 Re(conj(X^_k(f)) R_k(f))
+//   kbar2[a,b] = sum_f dL/ds2(f) 2 Re(conj(sigma(f)) exp(-2 pi i (a ky/H + b kx/W)))
+//   kbar1[a,b] = (1/HW) sum_f c(kx) Re(Z(f) exp(-2 pi i (ky (a-c)/H + kx (b-c)/W))),
+//                Z(f) = sum_p conj(Bbar_p(f)) Xin_p(f)
+// k_xspec forms sum_p conj(colFFT(U_p)) colFFT(V_p) per frequency from two sets of row
+// spectra, plane-group partials, with the packed column 0 split into kx = 0 and kx = N.
+// ---------------------------------------------------------------------------
+template <int H, int C, bool COL0>
+__global__ void __launch_bounds__(C * (H / RowCfg<H>::E), 1)
+    k_xspec(const cf* __restrict__ U, const cf* __restrict__ V, cf* __restrict__ part, const cf* __restrict__ twH_g,
+            int N, int colblocks, int P, int ppg) {
+    using G = ColGeom<H, C>;
+    constexpr int E = G::E, L = G::L;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* data = tw + H;
+    load_tw(tw, twH_g, H);
+    const int tid = threadIdx.x;
+    const int c = tid % C, t = tid / C;
+    const int ncb = COL0 ? 1 : colblocks - 1;
+    const int grp = blockIdx.x / ncb;
+    const int cb = COL0 ? 0 : 1 + (int)(blockIdx.x % ncb);
+    const int col = cb * C + c;
+    ColBuf<C> buf{data + c};
+    cf acc[E], accn[COL0 ? E : 1];
+#pragma unroll
+    for (int j = 0; j < E; ++j) acc[j] = mkc(0.f, 0.f);
+    if constexpr (COL0) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) accn[j] = mkc(0.f, 0.f);
+    }
+    __syncthreads();
+    const int p1 = min(P, (grp + 1) * ppg);
+    for (int p = grp * ppg; p < p1; ++p) {
+        const cf* up = U + (size_t)p * H * N + col;
+        const cf* vp = V + (size_t)p * H * N + col;
+        cf u[E], v[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) u[j] = up[(size_t)(t + L * j) * N];
+#pragma unroll
+        for (int j = 0; j < E; ++j) v[j] = vp[(size_t)(t + L * j) * N];
+        __syncthreads();  // previous plane's LDS reads are done
+        fft<H, L, -1, 1, 1>(u, buf, tw, t);
+        __syncthreads();
+        fft<H, L, -1, 1, 1>(v, buf, tw, t);
+        if constexpr (COL0) {
+            // split the packed (DC, Nyquist) column: A = (F + conj F~)/2, B = (F - conj F~)/(2i)
+            cf ua[E], ub[E];
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < E; ++j) buf.at(t + L * j) = u[j];
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const cf q = cconj(buf.at((H - (t + L * j)) & (H - 1)));
+                ua[j] = mkc(0.5f * (u[j].x + q.x), 0.5f * (u[j].y + q.y));
+                ub[j] = mkc(0.5f * (u[j].y - q.y), -0.5f * (u[j].x - q.x));
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < E; ++j) buf.at(t + L * j) = v[j];
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const cf q = cconj(buf.at((H - (t + L * j)) & (H - 1)));
+                const cf va = mkc(0.5f * (v[j].x + q.x), 0.5f * (v[j].y + q.y));
+                const cf vb = mkc(0.5f * (v[j].y - q.y), -0.5f * (v[j].x - q.x));
+                if (col == 0) {
+                    acc[j] = cadd(acc[j], cmulc(va, ua[j]));    // conj(uA) vA
+                    accn[j] = cadd(accn[j], cmulc(vb, ub[j]));  // conj(uB) vB
+                } else {
+                    acc[j] = cadd(acc[j], cmulc(v[j], u[j]));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < E; ++j) acc[j] = cadd(acc[j], cmulc(v[j], u[j]));
+        }
+    }
+    cf* out = part + (size_t)grp * (N + 1) * H;
+#pragma unroll
+    for (int j = 0; j < E; ++j) out[(size_t)col * H + t + L * j] = acc[j];
+    if constexpr (COL0) {
+        if (col == 0) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) out[(size_t)N * H + t + L * j] = accn[j];
+        }
+    }
+}
+
+// acc[f] += sum_g part[g][f] * (fcT ? fcT[f]^2 real part : complex), in fp64 (f over (N+1)*H)
+__global__ void k_xspec_reduce(const cf* __restrict__ part, int ngroups, long long nf, const float* __restrict__ fcT,
+                               double2* __restrict__ acc) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nf) return;
+    double re = 0.0, im = 0.0;
+    for (int g = 0; g < ngroups; ++g) {
+        const cf v = part[(size_t)g * nf + i];
+        re += v.x;
+        im += v.y;
+    }
+    if (fcT) {
+        const double f = fcT[i];
+        acc[i].x += f * f * re;  // only Re(conj(X^) R) enters dL/ds2
+    } else {
+        acc[i].x += re;
+        acc[i].y += im;
+    }
+}
+
+// kbar[a][b] (one block per tap) from A (fc^2-weighted, scaled sums), Z (scaled) and sigma.
+// Scalings: row spectra carry a factor 2, fc is stored / (2HW):
+//   A_true = (HW)^2 A,  Z_true = Z / 4.
+__global__ void k_psf_grad(const double2* __restrict__ A, const double2* __restrict__ Z,
+                           const double2* __restrict__ sigma, int k, int H, int W, float* __restrict__ gk) {
+    __shared__ double red[256];
+    const int tap = blockIdx.x;
+    const int a = tap / k, b = tap % k, c = k / 2;
+    const int N = W / 2;
+    const double HW = (double)H * W;
+    const long long nf = (long long)(N + 1) * H;
+    double acc = 0.0;
+    for (long long i = threadIdx.x; i < nf; i += blockDim.x) {
+        const int kx = (int)(i / H), ky = (int)(i % H);
+        const double cw = (kx == 0 || kx == N) ? 1.0 : 2.0;
+        double s, co;
+        // through fc: dL/ds2 * 2 Re(conj(sigma) e^{-2 pi i (a ky/H + b kx/W)})
+        const long long ph2 = ((long long)a * ky % H) * W + ((long long)b * kx % W) * H;  // units 1/(HW)
+        sincospi(2.0 * (double)(ph2 % (long long)HW) / HW, &s, &co);  // e^{-i t} = co - i s
+        const double2 sg = sigma[i];
+        const double dls2 = -HW * cw * A[i].x;
+        acc += dls2 * 2.0 * (sg.x * co - sg.y * s);  // Re(conj(sg) (co - i s)) = sg.x co - sg.y s
+        // through b = H_t(xin): (1/HW) c Re(Z_true e^{-2 pi i (ky (a-c)/H + kx (b-c)/W)})
+        long long ph1 = ((long long)(a - c) * ky) % H;
+        if (ph1 < 0) ph1 += H;
+        long long ph1x = ((long long)(b - c) * kx) % W;
+        if (ph1x < 0) ph1x += W;
+        const long long p1 = (ph1 * W + ph1x * H) % (long long)HW;
+        sincospi(2.0 * (double)p1 / HW, &s, &co);
+        const double2 z = Z[i];
+        acc += cw / HW * 0.25 * (z.x * co + z.y * s);  // Re((zx + i zy)(co - i s))
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) gk[tap] = (float)red[0];
+}
+
+}  // namespace admm

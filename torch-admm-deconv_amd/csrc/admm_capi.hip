@@ -88,7 +88,7 @@ constexpr size_t kAlign = 256;
 size_t up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Layout {
-    size_t spec[2], u[4], b, fcT, mT, twW, twH, twHd, G, part, nsq, total;
+    size_t spec[2], u[4], b, fcT, mT, twW, twH, twHd, G, part, nsq, sigma, total;
     int ngroups, ppg;
 };
 
@@ -113,6 +113,7 @@ Layout make_layout(const admm_tv_desc& d) {
     L.twH = take(H * sizeof(cf));
     L.twHd = take(H * sizeof(double2));
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
+    L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
         // plane groups for the iso norm pass: enough (group,row) items to fill the chip
         int ppg = 8;
@@ -238,50 +239,92 @@ template <class F> int with_row(int N, F&& f) {
 }
 
 // ------------------------------------------------------------------ column-side ops (templated on H, C)
-template <int H, int C> int pass_b_hc(cf* spec, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode,
-                                      hipStream_t s) {
+template <int H, int C> int pass_b_hc(const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N,
+                                      int P, int mode, hipStream_t s) {
     using G = ColGeom<H, C>;
     const int colblocks = N / C;
     const dim3 grid((unsigned)((long long)P * colblocks));
     if (mode == 0) {
         if (int e = set_lds(k_pass_b<H, C, 0>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, fcT, mT, twH, N, colblocks);
+        hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks);
     } else if (mode == 1) {
         if (int e = set_lds(k_pass_b<H, C, 1>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, fcT, mT, twH, N, colblocks);
+        hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks);
     } else {
         if (int e = set_lds(k_pass_b<H, C, 2>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, fcT, mT, twH, N, colblocks);
+        hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks);
     }
     return launch_check("k_pass_b");
 }
 
-template <int H> int pass_b_h(cf* spec, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode,
-                              hipStream_t s) {
+template <int H> int pass_b_h(const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N, int P,
+                              int mode, hipStream_t s) {
     constexpr int L = ColGeom<H, 1>::L;
     if constexpr (L <= 64) {
         int C = env_int("ADMM_PASSB_C", 8);
         if (C > N) C = N;
-        if (C >= 16) return pass_b_hc<H, 16>(spec, fcT, mT, twH, N, P, mode, s);
-        return pass_b_hc<H, 8>(spec, fcT, mT, twH, N, P, mode, s);
+        if (C >= 16) return pass_b_hc<H, 16>(spec, out, fcT, mT, twH, N, P, mode, s);
+        return pass_b_hc<H, 8>(spec, out, fcT, mT, twH, N, P, mode, s);
     } else if constexpr (L == 128) {
-        return pass_b_hc<H, 8>(spec, fcT, mT, twH, N, P, mode, s);
+        return pass_b_hc<H, 8>(spec, out, fcT, mT, twH, N, P, mode, s);
     } else {
-        return pass_b_hc<H, 4>(spec, fcT, mT, twH, N, P, mode, s);
+        return pass_b_hc<H, 4>(spec, out, fcT, mT, twH, N, P, mode, s);
+    }
+}
+
+// column pass; out == spec (in place) or a separate buffer
+int pass_b_oop(int H, const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode,
+               hipStream_t s) {
+    switch (H) {
+        case 16: return pass_b_h<16>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 32: return pass_b_h<32>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 64: return pass_b_h<64>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 128: return pass_b_h<128>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 256: return pass_b_h<256>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 512: return pass_b_h<512>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 1024: return pass_b_h<1024>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 2048: return pass_b_h<2048>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 4096: return pass_b_h<4096>(spec, out, fcT, mT, twH, N, P, mode, s);
+        default: return fail(ADMM_TV_EUNSUPPORTED, "unsupported H");
     }
 }
 
 int pass_b(int H, cf* spec, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode, hipStream_t s) {
+    return pass_b_oop(H, spec, spec, fcT, mT, twH, N, P, mode, s);
+}
+
+// cross-spectrum partials sum_{p in group} conj(colFFT U_p) colFFT V_p  -> part[g][N+1][H]
+template <int H, int C> int xspec_hc(const cf* U, const cf* V, cf* part, const cf* twH, int N, int P, int ppg,
+                                     hipStream_t s) {
+    using G = ColGeom<H, C>;
+    const int colblocks = N / C;
+    const int groups = (P + ppg - 1) / ppg;
+    if (int e = set_lds(k_xspec<H, C, true>, G::lds_bytes())) return e;
+    if (int e = set_lds(k_xspec<H, C, false>, G::lds_bytes())) return e;
+    hipLaunchKernelGGL((k_xspec<H, C, true>), dim3(groups), dim3(G::NT), G::lds_bytes(), s, U, V, part, twH, N,
+                       colblocks, P, ppg);
+    if (colblocks > 1)
+        hipLaunchKernelGGL((k_xspec<H, C, false>), dim3(groups * (colblocks - 1)), dim3(G::NT), G::lds_bytes(), s, U,
+                           V, part, twH, N, colblocks, P, ppg);
+    return launch_check("k_xspec");
+}
+template <int H> int xspec_h(const cf* U, const cf* V, cf* part, const cf* twH, int N, int P, int ppg, hipStream_t s) {
+    constexpr int L = ColGeom<H, 1>::L;
+    if constexpr (L <= 64) return xspec_hc<H, 8>(U, V, part, twH, N, P, ppg, s);
+    else if constexpr (L == 128) return xspec_hc<H, 8>(U, V, part, twH, N, P, ppg, s);
+    else return xspec_hc<H, 4>(U, V, part, twH, N, P, ppg, s);
+}
+int xspec(int H, const cf* U, const cf* V, cf* part, const cf* twH, int N, int P, int ppg, hipStream_t s) {
     switch (H) {
-        case 16: return pass_b_h<16>(spec, fcT, mT, twH, N, P, mode, s);
-        case 32: return pass_b_h<32>(spec, fcT, mT, twH, N, P, mode, s);
-        case 64: return pass_b_h<64>(spec, fcT, mT, twH, N, P, mode, s);
-        case 128: return pass_b_h<128>(spec, fcT, mT, twH, N, P, mode, s);
-        case 256: return pass_b_h<256>(spec, fcT, mT, twH, N, P, mode, s);
-        case 512: return pass_b_h<512>(spec, fcT, mT, twH, N, P, mode, s);
-        case 1024: return pass_b_h<1024>(spec, fcT, mT, twH, N, P, mode, s);
-        case 2048: return pass_b_h<2048>(spec, fcT, mT, twH, N, P, mode, s);
-        case 4096: return pass_b_h<4096>(spec, fcT, mT, twH, N, P, mode, s);
+        case 16: return xspec_h<16>(U, V, part, twH, N, P, ppg, s);
+        case 32: return xspec_h<32>(U, V, part, twH, N, P, ppg, s);
+        case 64: return xspec_h<64>(U, V, part, twH, N, P, ppg, s);
+        case 128: return xspec_h<128>(U, V, part, twH, N, P, ppg, s);
+        case 256: return xspec_h<256>(U, V, part, twH, N, P, ppg, s);
+        case 512: return xspec_h<512>(U, V, part, twH, N, P, ppg, s);
+        case 1024: return xspec_h<1024>(U, V, part, twH, N, P, ppg, s);
+        case 2048: return xspec_h<2048>(U, V, part, twH, N, P, ppg, s);
+        case 4096: return xspec_h<4096>(U, V, part, twH, N, P, ppg, s);
         default: return fail(ADMM_TV_EUNSUPPORTED, "unsupported H");
     }
 }
@@ -313,7 +356,8 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
     const int n = (N + 1) * H;
     if (rho) {
         hipLaunchKernelGGL(k_spectra, dim3((n + nt - 1) / nt), dim3(nt), 0, s, at<double2>(ws, Lo.G),
-                           at<double2>(ws, Lo.twHd), rho, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), k, H, N, W);
+                           at<double2>(ws, Lo.twHd), rho, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), k, H, N, W,
+                           Lo.sigma ? at<double2>(ws, Lo.sigma) : nullptr);
         if (int e = launch_check("k_spectra")) return e;
     }
     return 0;
@@ -352,6 +396,8 @@ struct Hist {
     size_t a_slot;     // bytes of one image
     size_t n_slot;     // bytes of one norm pair [2][H][W]
     size_t n_off;      // offset of the norm history
+    size_t t_off;      // offset of the r_k spectra (PSF gradient only)
+    bool keep_t;
     size_t total;
 };
 Hist make_hist(const admm_tv_desc& d) {
@@ -360,7 +406,9 @@ Hist make_hist(const admm_tv_desc& d) {
     h.a_slot = up(img);
     h.n_slot = d.iso ? up(2 * (size_t)d.H * d.W * sizeof(float)) : 0;
     h.n_off = (size_t)d.maxit * 2 * h.a_slot;
-    h.total = h.n_off + (size_t)d.maxit * h.n_slot;
+    h.t_off = h.n_off + (size_t)d.maxit * h.n_slot;
+    h.keep_t = d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD);
+    h.total = h.t_off + (h.keep_t ? (size_t)d.maxit * h.a_slot : 0);
     return h;
 }
 
@@ -395,6 +443,10 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     auto hn = [&](int k) -> float* {  // N_k (k >= 1)
         return reinterpret_cast<float*>(static_cast<char*>(hist) + Hs.n_off + (size_t)(k - 1) * Hs.n_slot);
     };
+    const bool keep_t = train && Hs.keep_t;
+    auto ht = [&](int k) -> cf* {  // r_k row spectra (k >= 1), kept for the PSF gradient
+        return reinterpret_cast<cf*>(static_cast<char*>(hist) + Hs.t_off + (size_t)(k - 1) * Hs.a_slot);
+    };
 
     // b = H_t(xin) once (the reference recomputes it every iteration, deconv.py:104)
     const float* bimg = xin;
@@ -406,7 +458,8 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     }
     {
         ProfScope ps(3, s);
-        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, spec[0], twW, rows, s); });
+        cf* t0 = keep_t ? ht(1) : spec[0];
+        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, t0, twW, rows, s); });
         if (e) return e;
     }
     const int R = strip_rows(H, N, rows);
@@ -415,7 +468,9 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     for (int it = 1; it <= d.maxit; ++it) {
         {
             ProfScope ps(1, s);
-            if (int e = pass_b(H, spec[cur], fcT, mT, twH, N, (int)P, 0, s)) return e;
+            // PSF-gradient training keeps r_k's spectrum: the column pass then runs out of place
+            const cf* tin = keep_t ? ht(it) : spec[cur];
+            if (int e = pass_b_oop(H, tin, spec[cur], fcT, mT, twH, N, (int)P, 0, s)) return e;
         }
         if (it == d.maxit) {
             ProfScope ps(3, s);
@@ -456,7 +511,8 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         }
         {
             ProfScope ps(0, s);
-            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, rows / R};
+            cf* tout = (keep_t && it < d.maxit) ? ht(it + 1) : spec[1 - cur];
+            PassAArgs pa{spec[cur], tout, bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, rows / R};
             int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, train, s); });
             if (e) return e;
         }
@@ -469,9 +525,9 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
 // backward workspace = forward layout + a^ ping-pong (4 images) + b^ + per-iteration partials
 struct BwdLayout {
     Layout f;
-    size_t abar[4], bbar, part, tpart, q, total;
+    size_t abar[4], bbar, part, tpart, q, xpart, aacc, zacc, total;
     long long nstrips;
-    int R, ntp;
+    int R, ntp, xgroups, xppg;
 };
 BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     BwdLayout B{};
@@ -492,6 +548,14 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     B.ntp = 256;
     B.tpart = take((size_t)std::max(d.maxit, 1) * B.ntp * sizeof(float));
     B.q = take(2 * (size_t)d.H * d.W * sizeof(float));
+    if (d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) {
+        const size_t nf = ((size_t)d.W / 2 + 1) * d.H;
+        B.xppg = 8;
+        B.xgroups = (int)((d.B * d.C + B.xppg - 1) / B.xppg);
+        B.xpart = take((size_t)B.xgroups * nf * sizeof(cf));
+        B.aacc = take(nf * sizeof(double2));
+        B.zacc = take(nf * sizeof(double2));
+    }
     B.total = o;
     return B;
 }
@@ -546,9 +610,9 @@ int admm_tv_backward_workspace_size(const admm_tv_desc* d, size_t* bytes) {
     return 0;
 }
 
-int admm_tv_backward(const admm_tv_desc* dp, const float* kern, const float* lam, const float* rho,
-                     const float* gout, const void* hist, size_t hist_bytes, float* gxin, float* glam, float* grho,
-                     void* ws, size_t ws_bytes, void* stream) {
+int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern, const float* lam,
+                     const float* rho, const float* gout, const void* hist, size_t hist_bytes, float* gxin,
+                     float* glam, float* grho, float* gkern, void* ws, size_t ws_bytes, void* stream) {
     if (int e = validate(dp)) return e;
     const admm_tv_desc d = *dp;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -560,10 +624,14 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* kern, const float* lam
     const long long P = d.B * d.C;
     const int H = (int)d.H, W = (int)d.W, N = W / 2, K = d.maxit;
     const size_t img_bytes = (size_t)P * H * W * sizeof(float);
+    const bool psf_grad = gkern != nullptr;
+    if (psf_grad && (d.kh == 0 || !(d.flags & ADMM_TV_FLAG_PSF_GRAD) || !xin))
+        return fail(ADMM_TV_EINVAL, "gkern needs a PSF, ADMM_TV_FLAG_PSF_GRAD (forward and backward) and xin");
     if (K == 0) {  // output is identically zero
         if (gxin) HIPCHK(hipMemsetAsync(gxin, 0, img_bytes, s));
         if (glam) HIPCHK(hipMemsetAsync(glam, 0, sizeof(float), s));
         if (grho) HIPCHK(hipMemsetAsync(grho, 0, sizeof(float), s));
+        if (gkern) HIPCHK(hipMemsetAsync(gkern, 0, sizeof(float) * d.kh * d.kw, s));
         return 0;
     }
     if (!hist || hist_bytes < make_hist(d).total) return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
@@ -574,6 +642,12 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* kern, const float* lam
         return reinterpret_cast<const float*>(hb + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
     };
     auto hn = [&](int k) -> const float* { return reinterpret_cast<const float*>(hb + Hs.n_off + (size_t)(k - 1) * Hs.n_slot); };
+    auto ht = [&](int k) -> const cf* { return reinterpret_cast<const cf*>(hb + Hs.t_off + (size_t)(k - 1) * Hs.a_slot); };
+    const long long nf = (long long)(N + 1) * H;
+    if (psf_grad) {
+        HIPCHK(hipMemsetAsync(at<double2>(ws, BL.aacc), 0, nf * sizeof(double2), s));
+        HIPCHK(hipMemsetAsync(at<double2>(ws, BL.zacc), 0, nf * sizeof(double2), s));
+    }
     cf* twW = at<cf>(ws, Lo.twW);
     cf* twH = at<cf>(ws, Lo.twH);
     float* fcT = at<float>(ws, Lo.fcT);
@@ -592,6 +666,12 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* kern, const float* lam
     if (e) return e;
     int cur = 0, ain = 0;
     for (int k = K; k >= 1; --k) {
+        if (psf_grad) {  // A += fc^2 Re(sum_p conj(X^_k) R_k), before the column pass rewrites X^_k
+            if ((e = xspec(H, spec[cur], ht(k), at<cf>(ws, BL.xpart), twH, N, (int)P, BL.xppg, s))) return e;
+            hipLaunchKernelGGL(k_xspec_reduce, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s,
+                               at<cf>(ws, BL.xpart), BL.xgroups, nf, fcT, at<double2>(ws, BL.aacc));
+            if ((e = launch_check("k_xspec_reduce"))) return e;
+        }
         {
             ProfScope ps(1, s);
             if ((e = pass_b(H, spec[cur], fcT, mT, twH, N, (int)P, 0, s))) return e;
@@ -634,6 +714,17 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* kern, const float* lam
     } else if (glam || grho) {
         return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
     }
+    if (psf_grad) {  // Z = sum_p conj(Bbar_p) Xin_p, then the k x k taps
+        if ((e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bbar, spec[0], twW, rows, s); }))) return e;
+        if ((e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(xin, spec[1], twW, rows, s); }))) return e;
+        if ((e = xspec(H, spec[0], spec[1], at<cf>(ws, BL.xpart), twH, N, (int)P, BL.xppg, s))) return e;
+        hipLaunchKernelGGL(k_xspec_reduce, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, at<cf>(ws, BL.xpart),
+                           BL.xgroups, nf, nullptr, at<double2>(ws, BL.zacc));
+        if ((e = launch_check("k_xspec_reduce"))) return e;
+        hipLaunchKernelGGL(k_psf_grad, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
+                           at<double2>(ws, BL.zacc), at<double2>(ws, Lo.sigma), d.kh, H, W, gkern);
+        if ((e = launch_check("k_psf_grad"))) return e;
+    }
     if (gxin && d.kh > 0) {
         // x^_in = H_t^T b^ : the conjugate multiplier (pass B mode 2)
         if ((e = psf_transpose_into(d, Lo, ws, bbar, gxin, spec[0], 2, s))) return e;
@@ -660,7 +751,7 @@ int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float*
     HIPCHK(hipMemsetAsync(at<float>(ws, Lo.fcT), 0, sizeof(float), s));
     hipLaunchKernelGGL(k_spectra, dim3((n + 255) / 256), dim3(256), 0, s, at<double2>(ws, Lo.G),
                        at<double2>(ws, Lo.twHd), at<float>(ws, Lo.fcT), at<float>(ws, Lo.spec[1]),
-                       at<cf>(ws, Lo.mT), d.kh, H, N, W);
+                       at<cf>(ws, Lo.mT), d.kh, H, N, W, nullptr);
     if (int e = launch_check("k_spectra")) return e;
     return psf_transpose_into(d, Lo, ws, xin, out, at<cf>(ws, Lo.spec[0]), 1, s);
 }

@@ -137,7 +137,7 @@ __global__ void k_psf_rows(const float* __restrict__ kern, double2* __restrict__
 // mT[kx][ky] = sigma * exp(+2 pi i c (ky/H + kx/W)) / (2HW)  (centred PSF, c = k/2)
 __global__ void k_spectra(const double2* __restrict__ G, const double2* __restrict__ twHd,
                           const float* __restrict__ rho_p, float* __restrict__ fcT, cf* __restrict__ mT, int k,
-                          int H, int N, int W) {
+                          int H, int N, int W, double2* __restrict__ sigma_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (N + 1) * H) return;
     const int kx = i / H, ky = i % H;
@@ -151,6 +151,7 @@ __global__ void k_spectra(const double2* __restrict__ G, const double2* __restri
             si += w.x * g.y + w.y * g.x;
         }
     }
+    if (sigma_out) sigma_out[i] = make_double2(sr, si);  // kept for the PSF gradient
     const double rho = (double)rho_p[0];
     const double sx = sinpi((double)kx / W), sy = sinpi((double)ky / H);
     const double lap = 4.0 * sx * sx + 4.0 * sy * sy;
@@ -254,7 +255,7 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
 
 template <int H, int C, int MODE>
 __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCfg<H>::E), sizeof(cf) * (H + (size_t)H * C)))
-    k_pass_b(cf* __restrict__ spec, const float* __restrict__ fcT, const cf* __restrict__ mT,
+    k_pass_b(const cf* spec_in, cf* spec_out, const float* __restrict__ fcT, const cf* __restrict__ mT,
              const cf* __restrict__ twH_g, int N, int colblocks) {
     using G = ColGeom<H, C>;
     constexpr int E = G::E, L = G::L;
@@ -268,7 +269,8 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
     const int p = lb / colblocks, cb = lb % colblocks;
     const int col = cb * C + c;
     // one plane of the spectrum = H*N*8 bytes (< 4 GiB); element (row, col) at (row*N + col)*8
-    const rsrc_t rs = make_rsrc(spec + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+    const rsrc_t rs = make_rsrc(spec_in + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+    const rsrc_t ro = make_rsrc(spec_out + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
     const int voff = (t * N + col) * (int)sizeof(cf);
     const int sstep = L * N * (int)sizeof(cf);
     cf v[E];
@@ -323,7 +325,7 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
     }
     fft<H, L, +1, 1, 1>(v, buf, tw, t);
 #pragma unroll
-    for (int j = 0; j < E; ++j) bstore_cf(rs, voff, j * sstep, v[j]);
+    for (int j = 0; j < E; ++j) bstore_cf(ro, voff, j * sstep, v[j]);
 }
 
 // ---------------------------------------------------------------------------
