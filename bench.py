@@ -39,6 +39,9 @@ CONFIGS = {
            "C2: batch-32 512x512x3, 15x15 motion PSF, lambda 0.01, rho 0.02, aniso, 50 iters"),
     "c5fwd": (16, 3, 512, 512, "none", 0, 100, True,
               "C5 forward (one ADMM module): batch-16 512x512x3, no PSF, iso, 100 iters"),
+    "c5": (16, 3, 512, 512, "none", 0, 100, True,
+           "C5 training step: DivergentRestorer([2,8,32],3,3,86,86,8, Sigmoid, 2 x ADMM-TV iso 100 it) "
+           "(scripts/train.py:70-73), batch-16 512x512x3, bf16 autocast, L1 loss, AdamW"),
 }
 
 # algorithmic HBM bytes per pixel per launch: pass A reads the x row
@@ -60,6 +63,8 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-planes", type=int, default=6, help="CPU baseline sample: planes of 1024^2")
     ap.add_argument("--cpu-iters", type=int, default=36, help="CPU baseline sample: timed iterations")
+    ap.add_argument("--c5-batch", type=int, default=None, help="C5 only: override the per-GPU batch")
+    ap.add_argument("--c5-no-ckpt", action="store_true", help="C5 only: keep all branch activations")
     return ap.parse_args()
 
 
@@ -118,6 +123,81 @@ def cpu_baseline(cfg, planes, iters):
                       f"value scaled by planes {nb * C}/{B * C}; CPU: {cpu}"}
 
 
+def run_c5(args, world, rank, dev):
+    """Config 5: one training step of the reference's training model
+    (scripts/train.py:70-73: two learnable iso ADMM-TV modules, 100 iterations each, then the
+    attention CNN), autograd through the HIP solver.  The reference trains with an SSIM-Lab loss
+    from its metrics package (out of scope); the step here uses L1 -- the loss is a few
+    elementwise ops next to the model.  N > 1: DDP over RCCL (gradient all-reduce, a real exchange
+    step), weak scaling (batch 16 per GPU)."""
+    from admmtor import _native
+    from admmtor.modelbuild.blocks import set_branch_checkpointing
+    from admmtor.modelbuild.denoiser import DivergentRestorer
+    from admmtor.synth import CONFIG_SEED, clean_images
+    B, C, H, W, _, _, maxit, _, desc = CONFIGS["c5"]
+    B = args.c5_batch or B
+    deconv = {"kern_size": (), "max_iters": maxit, "iso": True}
+    torch.manual_seed(CONFIG_SEED + 5)
+    model = DivergentRestorer([2, 8, 32], 3, 3, 86, 86, 8, output_activation=torch.nn.Sigmoid(),
+                              admms=[dict(deconv), dict(deconv)]).to(dev)
+    # the 8- and 32-branch levels recompute their branches in the backward (exact; without it the
+    # activations of batch 16 at 512^2 exceed 288 GB -- measured: OOM at 282 GiB allocated)
+    if not args.c5_no_ckpt:
+        set_branch_checkpointing(model, True)
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
+                                                          find_unused_parameters=True)
+    opt = torch.optim.AdamW(model.parameters(), 8.8e-4, betas=(0.9, 0.9))
+    y = clean_images(B, C, H, W, seed=CONFIG_SEED + 5 + 1000 * rank, device=dev)
+    g = torch.Generator(device=dev).manual_seed(CONFIG_SEED + 5 + rank)
+    x = (y + 0.06 * torch.randn(y.shape, generator=g, device=dev)).clamp_(0, 1)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+        loss = (out.float() - y).abs().mean()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _native.profile_reset()
+    _native.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    _native.profile_enable(False)
+    ms, cnt = _native.profile_read()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    T = elapsed.item()
+    K = args.steps
+    if rank == 0:
+        admm_ms = sum(ms)
+        print(json.dumps({
+            "metric": "C5 training steps/sec", "value": world * K / T, "unit": "steps/s", "n_gpus": world,
+            "steps": K, "warmup": args.warmup, "ms_per_step": T / K * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16 autocast (ADMM solve f32)",
+            "data": "synthetic (piecewise-constant shapes + AWGN 0.06, seeded per rank); random-init weights",
+            "config": {"workload": desc, "batch_per_gpu": B, "H": H, "W": W,
+                       "branch_checkpointing": not args.c5_no_ckpt,
+                       "parallelism": f"ddp{world}" if world > 1 else "single"},
+            "admm_share": {"ms_per_step_in_admm_kernels": admm_ms / K, "fraction": admm_ms / 1e3 / T,
+                           "launches_per_step": sum(cnt) / K},
+            "peak_mem_GiB": torch.cuda.max_memory_allocated(dev) / 2**30,
+            "loss": float(loss.detach()), "cpu_baseline": None}), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,6 +207,12 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
+    if args.config == "c5":
+        run_c5(args, world, rank, dev)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     cfg = CONFIGS[args.config]
     B, C, H, W, kind, k, maxit, iso, desc = cfg
 
