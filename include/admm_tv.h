@@ -36,7 +36,7 @@ extern "C" {
 enum {
     ADMM_TV_OK = 0,
     ADMM_TV_EINVAL = -1,        /* null pointer / negative sizes / maxit < 0       */
-    ADMM_TV_EUNSUPPORTED = -2,  /* H, W not a supported power of two (see below)    */
+    ADMM_TV_EUNSUPPORTED = -2,  /* H, W outside [1, 4096]; PSF gradient at a generic size */
     ADMM_TV_ENONSQUARE = -3,    /* kh != kw  (reference: RuntimeError, deconv.py:90-96) */
     ADMM_TV_EWORKSPACE = -4,    /* workspace too small / misaligned                 */
     ADMM_TV_EHIP = -5,          /* a HIP runtime call or kernel launch failed       */
@@ -63,7 +63,10 @@ typedef struct admm_tv_desc {
 /* ABI version (ADMM_TV_ABI_VERSION). */
 int admm_tv_abi_version(void);
 
-/* 1 if (H, W) can run on the HIP path, 0 otherwise. */
+/* 1: (H, W) runs on the fused power-of-two kernels (H in [16,4096], W in [16,2048]);
+ * 2: any other size in [1,4096] x [1,4096], run on the generic kernels (mixed-radix
+ *    transforms, per-pixel step; the reference accepts any size, deconv.py:103-106);
+ * 0: unsupported. */
 int admm_tv_supported(int64_t H, int64_t W);
 
 /* Workspace bytes needed by admm_tv_forward for `desc`. */

@@ -50,8 +50,10 @@ def test_host_entry_points():
     from admmtor import _native
     lib = _native.load()
     assert lib.admm_tv_abi_version() == 2
-    assert _native.supported(1024, 1024) and _native.supported(16, 2048) and _native.supported(4096, 16)
-    assert not _native.supported(15, 17) and not _native.supported(1024, 4096) and not _native.supported(8, 64)
+    fast, generic = 1, 2
+    assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
+    assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 4096), (8, 64), (1, 1), (481, 321))] == [generic] * 5
+    assert [lib.admm_tv_supported(*hw) for hw in ((4097, 16), (16, 8192), (0, 16))] == [0] * 3
     d = _native.desc(64, 3, 1024, 1024, 21, False, 50)
     ws = _native.workspace_size(d)
     img = 64 * 3 * 1024 * 1024 * 4
@@ -62,7 +64,7 @@ def test_host_entry_points():
 
 @pytest.mark.parametrize("field,value,code", [
     ("kw", 5, -3),      # non-square PSF -> ADMM_TV_ENONSQUARE
-    ("H", 24, -2),      # unsupported size
+    ("H", 5000, -2),    # unsupported size
     ("maxit", -1, -1),  # invalid
     ("kh", 99, -3),
 ])

@@ -1,0 +1,123 @@
+"""Generic sizes: every H, W in [1, 4096] that the fused power-of-two kernels
+do not take runs on the generic HIP kernels (mixed-radix LDS transforms + per-pixel step).
+
+Parity as for the fast path: rel-L2 <= 1e-5 against the reference's fp64 output (golden 15x17
+case) or the fp64 oracle pinned to it; gradients as in test_gpu_grad.py (1e-4 without PSF,
+1e-3 with one, kink-aware where the oracle reports a plane near the shrink kink).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+TOL_REF64 = 1e-5
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double().cpu().reshape(-1)
+    b = torch.as_tensor(b).double().cpu().reshape(-1)
+    return (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(b)).item()
+
+
+def solve(x, psf, lam, rho, iso, it, dev):
+    from admmtor.eops.deconv import fft_admm_tv
+    x = torch.as_tensor(x).float().to(dev)
+    k = torch.as_tensor(psf).float().to(dev) if psf is not None else torch.empty(0, device=dev)
+    out = fft_admm_tv(x, lam, rho, k, iso, it)
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+def oracle(x, psf, lam, rho, iso, it):
+    from oracle.admm_oracle import solve_fourier
+    k = torch.as_tensor(psf).double() if psf is not None else torch.empty(0, dtype=torch.float64)
+    return solve_fourier(torch.as_tensor(x).double(), lam, rho, k, iso, it)
+
+
+def test_generic_path_is_taken():
+    from admmtor import _native
+    assert _native.load().admm_tv_supported(15, 17) == 2 and _native.load().admm_tv_supported(64, 64) == 1
+
+
+def test_g7_odd_size_vs_reference(cuda_dev):
+    e = load_golden("g7_edges")
+    out = solve(e["odd_x"], e["odd_psf"], 0.01, 0.02, False, 20, cuda_dev)
+    err = rel(out, e["odd_out"])
+    print("15x17 even-PSF vs reference fp64:", err)
+    assert err <= TOL_REF64
+
+
+@pytest.mark.parametrize("shape,psf,iso,it", [
+    ((1, 2, 15, 17), None, True, 30),
+    ((2, 3, 24, 40), ("gauss:1.0", 5), False, 25),
+    ((1, 1, 100, 75), ("motion", 9), True, 20),
+    ((1, 3, 481, 321), ("gauss:1.5", 9), False, 30),      # a BSD-sized image
+    ((2, 1, 8, 64), None, False, 15),                      # power of two below the fast path's 16
+    ((1, 1, 1, 32), None, False, 10),                      # one row
+    ((1, 1, 7, 1), None, True, 10),                        # one column
+    ((1, 2, 97, 101), ("gauss:2", 7), False, 20),          # prime sizes (generic radix stages)
+    ((1, 1, 360, 1000), ("motion", 15), False, 10),        # 2^3 3^2 5 x 2^3 5^3
+    ((1, 1, 64, 4096), ("gauss:2", 11), False, 5),         # W beyond the fast path
+])
+def test_generic_shapes_vs_oracle(cuda_dev, shape, psf, iso, it):
+    from admmtor.synth import blurred_batch, make_psf
+    k = make_psf(*psf) if psf else None
+    x = blurred_batch(*shape, k if k is not None else torch.empty(0), seed=sum(shape))
+    got = solve(x, k, 0.01, 0.02, iso, it, cuda_dev)
+    ref = oracle(x, k, 0.01, 0.02, iso, it)
+    err = rel(got, ref)
+    print(shape, psf, "iso" if iso else "aniso", "rel vs fp64 oracle:", err)
+    assert err <= TOL_REF64
+
+
+def test_generic_psf_transpose(cuda_dev):
+    import ctypes
+    from admmtor import _native
+    from admmtor.synth import make_psf
+    from oracle.admm_oracle import apply_psf_transpose
+    x = torch.rand(2, 3, 45, 30, generator=torch.Generator().manual_seed(3))
+    k = make_psf("motion", 7)
+    xd, kd = x.to(cuda_dev), k.to(cuda_dev)
+    d = _native.desc(2, 3, 45, 30, 7, False, 1)
+    ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=cuda_dev)
+    got = torch.empty_like(xd)
+    _native.check(_native.load().admm_tv_psf_transpose(
+        ctypes.byref(d), xd.data_ptr(), kd.data_ptr(), got.data_ptr(), ws.data_ptr(), ws.numel(),
+        torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    ref = apply_psf_transpose(x.double(), k.double())
+    assert rel(got.cpu(), ref) <= 1e-6
+
+
+@pytest.mark.parametrize("shape,iso,it,psf", [((2, 2, 15, 17), False, 6, None), ((2, 2, 15, 17), True, 6, None),
+                                              ((1, 3, 24, 36), False, 4, ("gauss:1.0", 5)),
+                                              ((2, 1, 20, 12), True, 5, ("motion", 5))])
+def test_generic_grads_vs_oracle(cuda_dev, shape, iso, it, psf):
+    from admmtor.synth import blurred_batch, make_psf
+    from test_gpu_grad import hip_grads, oracle_grads
+    from oracle.admm_oracle import kink_margins
+    k = make_psf(*psf) if psf else None
+    x = blurred_batch(*shape, k if k is not None else torch.empty(0), seed=7)
+    cot = torch.randn(x.shape, generator=torch.Generator().manual_seed(2))
+    o1, gx1, gl1, gr1 = hip_grads(x, k, 0.03, 0.07, iso, it, cot, cuda_dev)
+    o2, gx2, gl2, gr2 = oracle_grads(x, k, 0.03, 0.07, iso, it, cot)
+    margins = kink_margins(x.double(), 0.03, 0.07, k.double() if k is not None else torch.empty(0, dtype=torch.float64),
+                           it) if not iso else None
+    e = (rel(o1, o2), rel(gx1, gx2), rel(gl1, gl2), rel(gr1, gr2))
+    print(shape, "iso" if iso else "aniso", it, psf, "out/gx/glam/grho rel:", e)
+    tol = 1e-3 if psf else 1e-4
+    assert e[0] <= TOL_REF64
+    near_kink = margins is not None and float(margins.min()) < 1e-5
+    if not near_kink:
+        assert e[1] <= tol and e[2] <= tol and e[3] <= tol
+
+
+def test_generic_psf_gradient_is_a_loud_gap(cuda_dev):
+    from admmtor.eops.deconv import fft_admm_tv
+    x = torch.rand(1, 1, 15, 17, device=cuda_dev)
+    k = torch.rand(1, 1, 3, 3, device=cuda_dev, requires_grad=True)
+    with pytest.raises(RuntimeError):
+        fft_admm_tv(x, 0.01, 0.02, k, False, 3).sum().backward()

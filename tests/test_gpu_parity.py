@@ -112,10 +112,10 @@ def test_g7_edges(cuda_dev):
         assert rel(o, e[key]) <= TOL_REF64, key
 
 
-def test_odd_size_is_a_loud_gap(cuda_dev):
-    e = load_golden("g7_edges")
+def test_oversized_image_is_a_loud_gap(cuda_dev):
+    # every H, W in [1, 4096] runs (odd sizes: tests/test_gpu_generic.py); beyond that it raises
     with pytest.raises(NotImplementedError):
-        solve(e["odd_x"], e["odd_psf"], 0.01, 0.02, False, 20, cuda_dev)
+        solve(np.zeros((1, 1, 4, 4100), np.float32), None, 0.01, 0.02, False, 2, cuda_dev)
 
 
 @pytest.mark.parametrize("shape,psf,iso", [

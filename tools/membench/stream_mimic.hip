@@ -1,0 +1,169 @@
+// Memory-system ceiling for pass A's access pattern (no FFT work): each wave walks a strip of
+// R rows of P planes x H x W floats, per row reading 4 row streams (spectrum, u_x, u_y, b) and
+// writing 3 (u_x, u_y, spectrum out), 8-byte accesses in the kernels' natural layout
+// (lane t, register j -> element t + 64 j).  Variants change only the stream structure.
+//   hipcc -O3 --offload-arch=gfx950 -o stream_mimic stream_mimic.hip && ./stream_mimic
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+typedef float2 cf;
+constexpr int W = 1024, N = 512, E = 8, L = 64;
+
+// 4 reads + 3 writes per row, pass A's layout
+template <class T> __device__ __forceinline__ void st(T* p, T v, bool nt) {
+    typedef float V __attribute__((ext_vector_type(sizeof(T) / 4)));
+    if (nt) __builtin_nontemporal_store(__builtin_bit_cast(V, v), reinterpret_cast<V*>(p)); else *p = v;
+}
+
+template <int R, bool NT = false>
+__global__ void __launch_bounds__(256) k_mimic(const cf* __restrict__ sp, const cf* __restrict__ uxi,
+                                               const cf* __restrict__ uyi, const cf* __restrict__ b,
+                                               cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
+                                               int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    cf acc[E];
+    for (int j = 0; j < E; ++j) acc[j] = sp[base + (size_t)((i0 - 1 + H) & (H - 1)) * N + t + L * j];
+    for (int rr = 0; rr <= R; ++rr) {
+        const size_t ro = base + (size_t)((i0 + rr) & (H - 1)) * N;
+        const size_t rm = base + (size_t)((i0 + rr - 1 + H) & (H - 1)) * N;
+        cf x[E], uy[E];
+        for (int j = 0; j < E; ++j) x[j] = sp[ro + t + L * j];
+        for (int j = 0; j < E; ++j) { uy[j] = uyi[ro + t + L * j]; uy[j].x += x[j].x; uy[j].y += acc[j].y; }
+        if (rr < R) for (int j = 0; j < E; ++j) st(&uyo[ro + t + L * j], uy[j], NT);
+        if (rr >= 1) {
+            for (int j = 0; j < E; ++j) { cf bb = b[rm + t + L * j]; acc[j].x += bb.x; acc[j].y -= bb.y; }
+            for (int j = 0; j < E; ++j) st(&so[rm + t + L * j], acc[j], NT);
+        }
+        if (rr < R) {
+            for (int j = 0; j < E; ++j) { cf u = uxi[ro + t + L * j]; u.x -= x[j].y; u.y += x[j].x; st(&uxo[ro + t + L * j], u, NT); }
+        }
+        for (int j = 0; j < E; ++j) acc[j] = x[j];
+    }
+}
+
+// u_x / u_y interleaved per row ([P][H][2][N] cf): 3 read + 2 write streams
+template <int R>
+__global__ void __launch_bounds__(256) k_mimic_il(const cf* __restrict__ sp, const cf* __restrict__ ui,
+                                                  const cf* __restrict__ b, cf* __restrict__ uo,
+                                                  cf* __restrict__ so, int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    cf acc[E];
+    for (int j = 0; j < E; ++j) acc[j] = sp[base + (size_t)((i0 - 1 + H) & (H - 1)) * N + t + L * j];
+    for (int rr = 0; rr <= R; ++rr) {
+        const size_t ro = base + (size_t)((i0 + rr) & (H - 1)) * N;
+        const size_t rm = base + (size_t)((i0 + rr - 1 + H) & (H - 1)) * N;
+        cf x[E], uy[E];
+        for (int j = 0; j < E; ++j) x[j] = sp[ro + t + L * j];
+        for (int j = 0; j < E; ++j) { uy[j] = ui[2 * ro + N + t + L * j]; uy[j].x += x[j].x; uy[j].y += acc[j].y; }
+        if (rr < R) for (int j = 0; j < E; ++j) uo[2 * ro + N + t + L * j] = uy[j];
+        if (rr >= 1) {
+            for (int j = 0; j < E; ++j) { cf bb = b[rm + t + L * j]; acc[j].x += bb.x; acc[j].y -= bb.y; }
+            for (int j = 0; j < E; ++j) so[rm + t + L * j] = acc[j];
+        }
+        if (rr < R) {
+            for (int j = 0; j < E; ++j) { cf u = ui[2 * ro + t + L * j]; u.x -= x[j].y; u.y += x[j].x; uo[2 * ro + t + L * j] = u; }
+        }
+        for (int j = 0; j < E; ++j) acc[j] = x[j];
+    }
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(256) k_copy(const float4* __restrict__ a, float4* __restrict__ o, size_t n) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) st(&o[i], a[i], NT);
+}
+// one float2 per thread, no loop (many blocks)
+template <bool NT>
+__global__ void __launch_bounds__(256) k_copy2(const float2* __restrict__ a, float2* __restrict__ o) {
+    const size_t i = blockIdx.x * 256ull + threadIdx.x;
+    st(&o[i], a[i], NT);
+}
+__global__ void __launch_bounds__(256) k_read(const float4* __restrict__ a, float* __restrict__ o, size_t n) {
+    float s = 0.f;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) { float4 v = a[i]; s += v.x + v.y + v.z + v.w; }
+    if (s == 12345.f) o[0] = s;
+}
+
+// pass B's access pattern: a block owns C adjacent columns of one plane (all H rows), thread
+// (c = tid % C, t = tid / C) moves element (t + L j, c), L = threads / C rows per step.
+template <int C, int TPB>
+__global__ void __launch_bounds__(TPB) k_colmimic(cf* __restrict__ spec, int H, int colblocks) {
+    constexpr int L = TPB / C;
+    const int c = threadIdx.x % C, t = threadIdx.x / C;
+    const int p = blockIdx.x / colblocks, cb = blockIdx.x % colblocks;
+    cf* base = spec + (size_t)p * H * N + cb * C + c;
+    const int E = H / L;
+    cf v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < E) v[j] = base[(size_t)(t + L * j) * N];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < E) { v[j].x *= 1.0001f; base[(size_t)(t + L * j) * N] = v[j]; }
+}
+
+int main() {
+    const int P = 192, H = 1024;
+    const size_t n = (size_t)P * H * N;  // cf per array
+    std::vector<cf*> buf(8);
+    for (auto& p : buf) { CK(hipMalloc(&p, n * sizeof(cf))); CK(hipMemset(p, 0, n * sizeof(cf))); }
+    cf *ui, *uo;
+    CK(hipMalloc(&ui, 2 * n * sizeof(cf))); CK(hipMalloc(&uo, 2 * n * sizeof(cf)));
+    CK(hipMemset(ui, 0, 2 * n * sizeof(cf)));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    auto timeit = [&](const char* name, double bytes, auto launch) {
+        for (int i = 0; i < 3; ++i) launch();
+        hipEventRecord(e0);
+        const int reps = 20;
+        for (int i = 0; i < reps; ++i) launch();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        ms /= reps;
+        printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+    };
+    const double arr = (double)n * sizeof(cf);
+    timeit("copy 1R+1W (float4, grid-stride 4096 blk)", 2 * arr, [&] { k_copy<false><<<4096, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
+    timeit("copy nt-store (float4, 4096 blk)", 2 * arr, [&] { k_copy<true><<<4096, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
+    timeit("copy (float4, 16384 blk)", 2 * arr, [&] { k_copy<false><<<16384, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
+    timeit("copy float2 1/thread", 2 * arr, [&] { k_copy2<false><<<(unsigned)(n / 256), 256>>>((const float2*)buf[0], (float2*)buf[1]); });
+    timeit("copy float2 1/thread nt", 2 * arr, [&] { k_copy2<true><<<(unsigned)(n / 256), 256>>>((const float2*)buf[0], (float2*)buf[1]); });
+    timeit("read only (float4)", arr, [&] { k_read<<<4096, 256>>>((const float4*)buf[0], (float*)buf[7], arr / 16); });
+    auto mimic = [&](auto kern, int R, const char* name) {
+        const long long ns = (long long)P * H / R;
+        const double bytes = 7 * arr;  // algorithmic: 4 reads + 3 writes
+        timeit(name, bytes, [&] { kern<<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+    };
+    mimic(k_mimic<8>, 8, "mimic 4R+3W R=8");
+    mimic(k_mimic<16>, 16, "mimic 4R+3W R=16");
+    mimic(k_mimic<4>, 4, "mimic 4R+3W R=4");
+    mimic(k_mimic<8, true>, 8, "mimic 4R+3W R=8 nt stores");
+    mimic(k_mimic<4, true>, 4, "mimic 4R+3W R=4 nt stores");
+    auto colm = [&](auto kern, int C, int tpb, const char* name) {
+        const int colblocks = N / C;
+        timeit(name, 2 * arr, [&] { kern<<<(unsigned)(P * colblocks), tpb>>>(buf[0], H, colblocks); });
+    };
+    colm(k_colmimic<8, 512>, 8, 512, "colmimic C=8  512 thr (E=16)");
+    colm(k_colmimic<16, 1024>, 16, 1024, "colmimic C=16 1024 thr (E=16)");
+    colm(k_colmimic<16, 512>, 16, 512, "colmimic C=16 512 thr (E=32)");
+    colm(k_colmimic<32, 1024>, 32, 1024, "colmimic C=32 1024 thr (E=32)");
+    colm(k_colmimic<8, 256>, 8, 256, "colmimic C=8  256 thr (E=32)");
+    {
+        const long long ns = (long long)P * H / 8;
+        timeit("mimic interleaved u 3R+2W R=8", 7 * arr, [&] { k_mimic_il<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], ui, buf[3], uo, buf[6], H, ns); });
+    }
+    return 0;
+}

@@ -117,9 +117,7 @@ def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.T
     k = int(k32.shape[-1]) if k32.numel() > 0 else 0
     d = _native.desc(B, C, H, W, k, iso, maxit)
     if not _native.supported(H, W):
-        raise NotImplementedError(
-            f"admmtor (MI355X build): H={H}, W={W} not supported yet by the HIP FFT passes "
-            "(H: power of two in [16, 4096], W: power of two in [16, 2048])")
+        raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} outside [1, 4096]")
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
     out = torch.empty_like(x32)
     stream = torch.cuda.current_stream(x32.device).cuda_stream

@@ -13,7 +13,7 @@
 #include <type_traits>
 #include <vector>
 
-#include "admm_backward.hpp"
+#include "generic_kernels.hpp"
 #include "admm_tv.h"
 
 using namespace admm;
@@ -80,8 +80,14 @@ struct AllReduce {
 // ------------------------------------------------------------------ geometry
 bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 
+// fused power-of-two kernels
 bool supported_hw(int64_t H, int64_t W) {
     return pow2(H) && pow2(W) && H >= 16 && H <= 4096 && W >= 16 && W <= 2048;
+}
+// any other size up to 4096 x 4096 runs on the generic kernels (generic_kernels.hpp)
+constexpr int64_t kGenericMax = 4096;
+bool generic_hw(int64_t H, int64_t W) {
+    return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax;
 }
 
 constexpr size_t kAlign = 256;
@@ -89,7 +95,9 @@ size_t up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Layout {
     size_t spec[2], u[4], b, fcT, mT, twW, twH, twHd, G, part, nsq, sigma, total;
+    size_t rimg;  // generic path: spec[0] = half spectra [P][H][W/2+1], spec[1] = x image, rimg = r image
     int ngroups, ppg;
+    bool gen;
 };
 
 Layout make_layout(const admm_tv_desc& d) {
@@ -103,8 +111,10 @@ Layout make_layout(const admm_tv_desc& d) {
         o += up(bytes);
         return at;
     };
-    L.spec[0] = take(img);
+    L.gen = generic_hw(d.H, d.W);
+    L.spec[0] = take(L.gen ? P * H * (N + 1) * sizeof(cf) : img);
     L.spec[1] = take(img);
+    L.rimg = L.gen ? take(img) : 0;
     for (int i = 0; i < 4; ++i) L.u[i] = take(img);
     L.b = k > 0 ? take(img) : 0;
     L.fcT = take((N + 1) * H * sizeof(float));
@@ -334,10 +344,18 @@ int validate(const admm_tv_desc* d) {
     if (d->B <= 0 || d->C <= 0 || d->H <= 0 || d->W <= 0 || d->maxit < 0 || d->kh < 0 || d->kw < 0)
         return fail(ADMM_TV_EINVAL, "invalid sizes or maxit");
     if (d->kh != d->kw) return fail(ADMM_TV_ENONSQUARE, "non-square PSF (the reference's H_t swaps H/W pads)");
-    if (!supported_hw(d->H, d->W))
-        return fail(ADMM_TV_EUNSUPPORTED, "H must be a power of two in [16,4096] and W a power of two in [16,2048]");
+    if (!supported_hw(d->H, d->W) && !generic_hw(d->H, d->W))
+        return fail(ADMM_TV_EUNSUPPORTED, "H and W must be in [1, 4096]");
     if (d->kh > d->H || d->kw > d->W) return fail(ADMM_TV_EKERNEL, "PSF larger than the image");
+    if (generic_hw(d->H, d->W) && d->kh > 0 && (d->flags & ADMM_TV_FLAG_PSF_GRAD))
+        return fail(ADMM_TV_EUNSUPPORTED, "PSF gradient needs power-of-two H, W in this build");
     return 0;
+}
+
+// the multiplier tables carry the transforms' normalisation: the packed power-of-two row
+// transforms produce 2 rfft, the generic ones rfft
+double spectra_scale(int H, int W) {
+    return (supported_hw(H, W) ? 0.5 : 1.0) / ((double)H * (double)W);
 }
 
 // setup: twiddle tables, PSF spectrum, Wiener factor (if rho given), centred-PSF multiplier
@@ -357,7 +375,7 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
     if (rho) {
         hipLaunchKernelGGL(k_spectra, dim3((n + nt - 1) / nt), dim3(nt), 0, s, at<double2>(ws, Lo.G),
                            at<double2>(ws, Lo.twHd), rho, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), k, H, N, W,
-                           Lo.sigma ? at<double2>(ws, Lo.sigma) : nullptr);
+                           Lo.sigma ? at<double2>(ws, Lo.sigma) : nullptr, spectra_scale(H, W));
         if (int e = launch_check("k_spectra")) return e;
     }
     return 0;
@@ -391,6 +409,117 @@ int psf_transpose_into(const admm_tv_desc& d, const Layout& Lo, void* ws, const 
     return with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec, bb, twW, rows, s); });
 }
 
+
+// ------------------------------------------------------------------ generic sizes (generic_kernels.hpp)
+GPlan make_plan(int n) {
+    GPlan p{};
+    p.n = n;
+    int m = n;
+    auto take_all = [&](int r) {
+        while (m % r == 0 && m > 1) {
+            p.rad[p.nst++] = r;
+            m /= r;
+        }
+    };
+    take_all(4);
+    take_all(2);
+    take_all(3);
+    take_all(5);
+    take_all(7);
+    for (int f = 11; m > 1; f += 2) take_all(f);  // any other prime: O(R) per output
+    return p;
+}
+
+// rows per block of the row transforms / columns per block of the column pass, sized so the
+// LDS image (twiddles + two ping-pong buffers) stays within 96 KB
+int grow_lines(int W) { return std::max(1, std::min(32, (12288 / W - 1) / 2)); }
+int gcol_cols(int H) { return std::max(1, std::min(16, (12288 / H - 1) / 2)); }
+
+int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hipStream_t s) {
+    GRowArgs a{img, spec, nullptr, tw, make_plan(W), rows, grow_lines(W)};
+    const size_t lds = sizeof(cf) * (size_t)W * (1 + 2 * a.lines);
+    if (int e = set_lds(k_grow_fwd, lds)) return e;
+    hipLaunchKernelGGL(k_grow_fwd, dim3((unsigned)((rows + a.lines - 1) / a.lines)), dim3(256), lds, s, a);
+    return launch_check("k_grow_fwd");
+}
+int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hipStream_t s) {
+    GRowArgs a{nullptr, const_cast<cf*>(spec), img, tw, make_plan(W), rows, grow_lines(W)};
+    const size_t lds = sizeof(cf) * (size_t)W * (1 + 2 * a.lines);
+    if (int e = set_lds(k_grow_inv, lds)) return e;
+    hipLaunchKernelGGL(k_grow_inv, dim3((unsigned)((rows + a.lines - 1) / a.lines)), dim3(256), lds, s, a);
+    return launch_check("k_grow_inv");
+}
+int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H, int W, long long P, int mode,
+         hipStream_t s) {
+    const int Wh = W / 2 + 1, cols = gcol_cols(H);
+    const int colblocks = (Wh + cols - 1) / cols;
+    GColArgs a{spec, dump, fcT, mT, tw, make_plan(H), Wh, cols, colblocks, P};
+    const size_t lds = sizeof(cf) * (size_t)H * (1 + 2 * cols);
+    const dim3 grid((unsigned)(P * colblocks));
+    switch (mode) {
+        case 0:
+            if (int e = set_lds(k_gcol<0>, lds)) return e;
+            hipLaunchKernelGGL(k_gcol<0>, grid, dim3(256), lds, s, a);
+            break;
+        case 1:
+            if (int e = set_lds(k_gcol<1>, lds)) return e;
+            hipLaunchKernelGGL(k_gcol<1>, grid, dim3(256), lds, s, a);
+            break;
+        case 2:
+            if (int e = set_lds(k_gcol<2>, lds)) return e;
+            hipLaunchKernelGGL(k_gcol<2>, grid, dim3(256), lds, s, a);
+            break;
+        default:
+            if (int e = set_lds(k_gcol<3>, lds)) return e;
+            hipLaunchKernelGGL(k_gcol<3>, grid, dim3(256), lds, s, a);
+            break;
+    }
+    return launch_check("k_gcol");
+}
+// img_out = real part of the 2-D transform chain  rowFFT -> column pass (mode) -> rowIFFT  of img_in
+int gapply(const float* img_in, float* img_out, cf* spec, const Layout& Lo, void* ws, const admm_tv_desc& d, int mode,
+           hipStream_t s) {
+    const long long P = d.B * d.C, rows = P * d.H;
+    const int H = (int)d.H, W = (int)d.W;
+    cf* twW = at<cf>(ws, Lo.twW);
+    if (int e = grow_fwd(img_in, spec, twW, W, rows, s)) return e;
+    if (int e = gcol(spec, nullptr, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), at<cf>(ws, Lo.twH), H, W, P, mode, s))
+        return e;
+    return grow_inv(spec, img_out, twW, W, rows, s);
+}
+
+int gstep(const GStepArgs& a, bool iso, bool first, bool hist, hipStream_t s) {
+    const dim3 grid((unsigned)((a.npx + 255) / 256)), blk(256);
+    const int sel = (iso ? 4 : 0) | (first ? 2 : 0) | (hist ? 1 : 0);
+    switch (sel) {
+        case 0: hipLaunchKernelGGL((k_gstep<false, false, false>), grid, blk, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_gstep<false, false, true>), grid, blk, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_gstep<false, true, false>), grid, blk, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_gstep<false, true, true>), grid, blk, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_gstep<true, false, false>), grid, blk, 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_gstep<true, false, true>), grid, blk, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_gstep<true, true, false>), grid, blk, 0, s, a); break;
+        default: hipLaunchKernelGGL((k_gstep<true, true, true>), grid, blk, 0, s, a); break;
+    }
+    return launch_check("k_gstep");
+}
+
+int gbwd(const GBwdArgs& a, bool iso, bool lastk, bool firstk, hipStream_t s) {
+    const dim3 grid((unsigned)((a.npx + 255) / 256)), blk(256);
+    const int sel = (iso ? 4 : 0) | (lastk ? 2 : 0) | (firstk ? 1 : 0);
+    switch (sel) {
+        case 0: hipLaunchKernelGGL((k_gbwd<false, false, false>), grid, blk, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_gbwd<false, false, true>), grid, blk, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_gbwd<false, true, false>), grid, blk, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_gbwd<false, true, true>), grid, blk, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_gbwd<true, false, false>), grid, blk, 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_gbwd<true, false, true>), grid, blk, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_gbwd<true, true, false>), grid, blk, 0, s, a); break;
+        default: hipLaunchKernelGGL((k_gbwd<true, true, true>), grid, blk, 0, s, a); break;
+    }
+    return launch_check("k_gbwd");
+}
+
 // history (training) storage: a_k for k = 1..K (x and y images), iso norms N_k
 struct Hist {
     size_t a_slot;     // bytes of one image
@@ -412,6 +541,93 @@ Hist make_hist(const admm_tv_desc& d) {
     return h;
 }
 
+
+// generic-size forward (same contract as run_forward; generic_kernels.hpp)
+int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, const float* lam, const float* rho,
+                    float* out, void* ws, void* hist, hipStream_t s) {
+    const long long P = d.B * d.C;
+    const int H = (int)d.H, W = (int)d.W;
+    const long long rows = P * H, npx = rows * W;
+    cf* twW = at<cf>(ws, Lo.twW);
+    cf* twH = at<cf>(ws, Lo.twH);
+    float* fcT = at<float>(ws, Lo.fcT);
+    cf* mT = at<cf>(ws, Lo.mT);
+    cf* spec = at<cf>(ws, Lo.spec[0]);
+    float* ximg = at<float>(ws, Lo.spec[1]);
+    float* rimg = at<float>(ws, Lo.rimg);
+    float* u[4] = {at<float>(ws, Lo.u[0]), at<float>(ws, Lo.u[1]), at<float>(ws, Lo.u[2]), at<float>(ws, Lo.u[3])};
+    const bool train = hist != nullptr;
+    const Hist Hs = make_hist(d);
+    auto ha = [&](int k, int comp) -> float* {
+        return reinterpret_cast<float*>(static_cast<char*>(hist) + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
+    };
+    auto hn = [&](int k) -> float* {
+        return reinterpret_cast<float*>(static_cast<char*>(hist) + Hs.n_off + (size_t)(k - 1) * Hs.n_slot);
+    };
+    const float* bimg = xin;
+    if (d.kh > 0) {  // b = H_t(xin) once
+        ProfScope ps(3, s);
+        float* bb = at<float>(ws, Lo.b);
+        if (int e = gapply(xin, bb, spec, Lo, ws, d, 1, s)) return e;
+        bimg = bb;
+    }
+    {
+        ProfScope ps(3, s);
+        if (int e = grow_fwd(bimg, spec, twW, W, rows, s)) return e;  // r_1 = b
+    }
+    int uin = 0;
+    for (int it = 1; it <= d.maxit; ++it) {
+        const bool last = it == d.maxit;
+        {
+            ProfScope ps(1, s);
+            if (int e = gcol(spec, nullptr, fcT, mT, twH, H, W, P, 0, s)) return e;
+            if (int e = grow_inv(spec, last ? out : ximg, twW, W, rows, s)) return e;
+        }
+        if (last && !train) break;
+        const float* xk = last ? out : ximg;
+        const bool first = it == 1;
+        const float *uxi, *uyi, *nprev = nullptr;
+        float *uxo, *uyo;
+        if (train) {
+            uxi = first ? nullptr : ha(it - 1, 0);
+            uyi = first ? nullptr : ha(it - 1, 1);
+            uxo = ha(it, 0);
+            uyo = ha(it, 1);
+            if (d.iso && !first) nprev = hn(it - 1);
+        } else {
+            uxi = u[2 * uin];
+            uyi = u[2 * uin + 1];
+            uxo = u[2 * (1 - uin)];
+            uyo = u[2 * (1 - uin) + 1];
+        }
+        const float* nsq = nullptr;
+        if (d.iso) {
+            ProfScope ps(2, s);
+            float* nout = train ? hn(it) : at<float>(ws, Lo.nsq);
+            const long long hw = (long long)H * W;
+            const dim3 grid((unsigned)((hw + 255) / 256)), blk(256);
+            if (first)
+                hipLaunchKernelGGL((k_giso_norm<true, false>), grid, blk, 0, s, xk, uxi, uyi, nprev, lam, rho, nout, H, W, P);
+            else if (train)
+                hipLaunchKernelGGL((k_giso_norm<false, true>), grid, blk, 0, s, xk, uxi, uyi, nprev, lam, rho, nout, H, W, P);
+            else
+                hipLaunchKernelGGL((k_giso_norm<false, false>), grid, blk, 0, s, xk, uxi, uyi, nprev, lam, rho, nout, H, W, P);
+            if (int e = launch_check("k_giso_norm")) return e;
+            if (g_allreduce.fn) g_allreduce.fn(nout, 2ull * H * W, s, g_allreduce.ctx);
+            nsq = nout;
+        }
+        {
+            ProfScope ps(0, s);
+            GStepArgs ga{xk, bimg, uxi, uyi, uxo, uyo, last ? nullptr : rimg, nsq, nprev, lam, rho, H, W, npx};
+            if (int e = gstep(ga, d.iso != 0, first, train, s)) return e;
+            if (!last)
+                if (int e = grow_fwd(rimg, spec, twW, W, rows, s)) return e;
+        }
+        uin = 1 - uin;
+    }
+    return 0;
+}
+
 // The forward solver.  hist == nullptr: inference (u ping-pong).  Otherwise training mode:
 // a_k -> hist slot k-1 (x image at 2(k-1), y image at 2(k-1)+1), N_k -> norm slot k-1, and
 // the last iteration's pass A also runs (a_K is needed by the backward).
@@ -428,6 +644,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         return 0;
     }
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
+    if (Lo.gen) return run_forward_gen(d, Lo, xin, lam, rho, out, ws, hist, s);
     cf* twW = at<cf>(ws, Lo.twW);
     cf* twH = at<cf>(ws, Lo.twH);
     float* fcT = at<float>(ws, Lo.fcT);
@@ -542,8 +759,13 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     for (int i = 0; i < 4; ++i) B.abar[i] = take(img);
     B.bbar = take(img);
     const long long rows = d.B * d.C * d.H;
-    B.R = strip_rows((int)d.H, (int)d.W / 2, rows);
-    B.nstrips = rows / B.R;
+    if (B.f.gen) {  // generic backward: one partial pair per 256-pixel block
+        B.R = 0;
+        B.nstrips = (rows * d.W + 255) / 256;
+    } else {
+        B.R = strip_rows((int)d.H, (int)d.W / 2, rows);
+        B.nstrips = rows / B.R;
+    }
     B.part = take((size_t)std::max(d.maxit, 1) * B.nstrips * 2 * sizeof(float));
     B.ntp = 256;
     B.tpart = take((size_t)std::max(d.maxit, 1) * B.ntp * sizeof(float));
@@ -560,6 +782,80 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     return B;
 }
 
+
+// generic-size backward (same contract as admm_tv_backward, PSF gradient excluded)
+int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* lam, const float* rho, const float* gout,
+                     const void* hist, float* gxin, float* glam, float* grho, void* ws, hipStream_t s) {
+    const Layout& Lo = BL.f;
+    const long long P = d.B * d.C;
+    const int H = (int)d.H, W = (int)d.W, K = d.maxit;
+    const long long npx = P * H * W;
+    const long long HW = (long long)H * W;
+    const Hist Hs = make_hist(d);
+    char* hb = static_cast<char*>(const_cast<void*>(hist));
+    auto ha = [&](int k, int comp) -> const float* {
+        return reinterpret_cast<const float*>(hb + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
+    };
+    auto hn = [&](int k) -> const float* { return reinterpret_cast<const float*>(hb + Hs.n_off + (size_t)(k - 1) * Hs.n_slot); };
+    cf* spec = at<cf>(ws, Lo.spec[0]);
+    float* rb = at<float>(ws, Lo.spec[1]);   // r^_k
+    float* xbuf[2] = {at<float>(ws, Lo.rimg), at<float>(ws, Lo.u[0])};  // x^ ping-pong
+    float* ab[4] = {at<float>(ws, BL.abar[0]), at<float>(ws, BL.abar[1]), at<float>(ws, BL.abar[2]),
+                    at<float>(ws, BL.abar[3])};
+    float* bbar = (d.kh == 0 && gxin) ? gxin : at<float>(ws, BL.bbar);
+    float* part = at<float>(ws, BL.part);
+    float* tpart = at<float>(ws, BL.tpart);
+    float* q = at<float>(ws, BL.q);
+    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * BL.ntp * sizeof(float), s));
+    const float* xbk = gout;
+    int ain = 0, xo = 0;
+    for (int k = K; k >= 1; --k) {
+        const bool lastk = (k == K), firstk = (k == 1);
+        {
+            ProfScope ps(1, s);
+            if (int e = gapply(xbk, rb, spec, Lo, ws, d, 0, s)) return e;  // r^_k = M x^_k
+        }
+        if (d.iso && !firstk) {
+            ProfScope ps(2, s);
+            const dim3 grid((unsigned)((HW + 255) / 256)), blk(256);
+            if (lastk)
+                hipLaunchKernelGGL(k_giso_q<true>, grid, blk, 0, s, rb, ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0),
+                                   ha(k - 1, 1), rho, q, H, W, P);
+            else
+                hipLaunchKernelGGL(k_giso_q<false>, grid, blk, 0, s, rb, ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0),
+                                   ha(k - 1, 1), rho, q, H, W, P);
+            if (int e = launch_check("k_giso_q")) return e;
+            hipLaunchKernelGGL(k_iso_tau_partial, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
+                               tpart + (size_t)(K - k) * BL.ntp, 2LL * HW);
+            if (int e = launch_check("k_iso_tau_partial")) return e;
+            if (g_allreduce.fn) g_allreduce.fn(q, 2ull * H * W, s, g_allreduce.ctx);
+        }
+        {
+            ProfScope ps(0, s);
+            GBwdArgs ba{rb, xbuf[xo], bbar,
+                        ab[2 * ain], ab[2 * ain + 1], ab[2 * (1 - ain)], ab[2 * (1 - ain) + 1],
+                        ha(k, 0), ha(k, 1),
+                        firstk ? nullptr : ha(k - 1, 0), firstk ? nullptr : ha(k - 1, 1),
+                        (d.iso && !firstk) ? hn(k - 1) : nullptr, q, lam, rho,
+                        part + (size_t)(K - k) * BL.nstrips * 2, H, W, npx};
+            if (int e = gbwd(ba, d.iso != 0, lastk, firstk, s)) return e;
+        }
+        xbk = xbuf[xo];
+        xo = 1 - xo;
+        ain = 1 - ain;
+    }
+    if (glam && grho) {
+        hipLaunchKernelGGL(k_bwd_scalars, dim3(1), dim3(256), 0, s, part, (long long)K * BL.nstrips, tpart,
+                           d.iso ? K * BL.ntp : 0, lam, rho, glam, grho);
+        if (int e = launch_check("k_bwd_scalars")) return e;
+    } else if (glam || grho) {
+        return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
+    }
+    if (gxin && d.kh > 0)  // x^_in = H_t^T b^
+        if (int e = gapply(bbar, gxin, spec, Lo, ws, d, 2, s)) return e;
+    return 0;
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -567,7 +863,7 @@ extern "C" {
 
 int admm_tv_abi_version(void) { return ADMM_TV_ABI_VERSION; }
 
-int admm_tv_supported(int64_t H, int64_t W) { return supported_hw(H, W) ? 1 : 0; }
+int admm_tv_supported(int64_t H, int64_t W) { return supported_hw(H, W) ? 1 : generic_hw(H, W) ? 2 : 0; }
 
 const char* admm_tv_last_error(void) { return g_err.c_str(); }
 
@@ -636,6 +932,10 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     }
     if (!hist || hist_bytes < make_hist(d).total) return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
+    if (Lo.gen) {
+        if (psf_grad) return fail(ADMM_TV_EUNSUPPORTED, "PSF gradient needs power-of-two H, W in this build");
+        return run_backward_gen(d, BL, lam, rho, gout, hist, gxin, glam, grho, ws, s);
+    }
     const Hist Hs = make_hist(d);
     char* hb = static_cast<char*>(const_cast<void*>(hist));
     auto ha = [&](int k, int comp) -> const float* {
@@ -751,8 +1051,9 @@ int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float*
     HIPCHK(hipMemsetAsync(at<float>(ws, Lo.fcT), 0, sizeof(float), s));
     hipLaunchKernelGGL(k_spectra, dim3((n + 255) / 256), dim3(256), 0, s, at<double2>(ws, Lo.G),
                        at<double2>(ws, Lo.twHd), at<float>(ws, Lo.fcT), at<float>(ws, Lo.spec[1]),
-                       at<cf>(ws, Lo.mT), d.kh, H, N, W, nullptr);
+                       at<cf>(ws, Lo.mT), d.kh, H, N, W, nullptr, spectra_scale(H, W));
     if (int e = launch_check("k_spectra")) return e;
+    if (Lo.gen) return gapply(xin, out, at<cf>(ws, Lo.spec[0]), Lo, ws, d, 1, s);
     return psf_transpose_into(d, Lo, ws, xin, out, at<cf>(ws, Lo.spec[0]), 1, s);
 }
 

@@ -133,11 +133,12 @@ __global__ void k_psf_rows(const float* __restrict__ kern, double2* __restrict__
     G[i] = make_double2(re, im);
 }
 
-// fcT[kx][ky] = 1 / (|sigma|^2 + rho (|Dx^|^2 + |Dy^|^2)) / (2HW);
-// mT[kx][ky] = sigma * exp(+2 pi i c (ky/H + kx/W)) / (2HW)  (centred PSF, c = k/2)
+// fcT[kx][ky] = scale / (|sigma|^2 + rho (|Dx^|^2 + |Dy^|^2));
+// mT[kx][ky] = scale * sigma * exp(+2 pi i c (ky/H + kx/W))  (centred PSF, c = k/2)
+// scale = 1/(2HW) for the packed power-of-two path, 1/(HW) for the generic path
 __global__ void k_spectra(const double2* __restrict__ G, const double2* __restrict__ twHd,
                           const float* __restrict__ rho_p, float* __restrict__ fcT, cf* __restrict__ mT, int k,
-                          int H, int N, int W, double2* __restrict__ sigma_out) {
+                          int H, int N, int W, double2* __restrict__ sigma_out, double scale) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (N + 1) * H) return;
     const int kx = i / H, ky = i % H;
@@ -155,7 +156,6 @@ __global__ void k_spectra(const double2* __restrict__ G, const double2* __restri
     const double rho = (double)rho_p[0];
     const double sx = sinpi((double)kx / W), sy = sinpi((double)ky / H);
     const double lap = 4.0 * sx * sx + 4.0 * sy * sy;
-    const double scale = 1.0 / (2.0 * (double)H * (double)W);
     fcT[i] = (float)(scale / (sr * sr + si * si + rho * lap));
     if (k > 0) {
         const int c = k / 2;  // ceil((k-1)/2): anchor of the reference's H_t
@@ -361,6 +361,9 @@ struct PassAArgs {
 #define PASSA_MINW_SMALL 3
 #endif
 #define PASSA_MINW(n) ((n) >= 1024 ? 1 : PASSA_MINW_SMALL)
+#ifndef PASSA_PF
+#define PASSA_PF 0
+#endif
 
 template <bool ISO> __device__ __forceinline__ float shrink_z(float a, float tau, float nsum) {
     if constexpr (ISO) return block_factor(nsum, tau) * a;
@@ -415,28 +418,73 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
     const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev);
     const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + (size_t)H * W);
 
-    cf xprev[E], xcur[E], wxp[E], wyp[E];
+    // Loads are issued ahead of the transforms that precede their use (PASSA_PF): the LDS
+    // fences inside the FFTs keep the compiler from hoisting them itself, so without this
+    // every load group waits a full HBM round trip right before it is consumed.
+    //   PF >= 1: the next row's spectrum is loaded while the current row is processed
+    //   PF >= 2: u_y / u_x of the current row are loaded before its c2r
+    //   PF >= 3: b of the row being finalised is loaded before the c2r
+    constexpr int PF = PASSA_PF;
+    cf xprev[E], xcur[E], wxp[E], wyp[E], xnext[E];
     {
         const int g = (i0 - 1 + H) & (H - 1);
 #pragma unroll
         for (int j = 0; j < E; ++j) xprev[j] = sp[(size_t)g * N + t + L * j];
+        if constexpr (PF >= 1) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) xnext[j] = sp[(size_t)(i0 & (H - 1)) * N + t + L * j];
+        }
         RowXf<N>::c2r(xprev, buf, tw, t);
     }
     for (int rr = 0; rr <= R; ++rr) {
         const int g = (i0 + rr) & (H - 1);
         const size_t ro = (size_t)g * N;  // row offset in cf units (spectrum and pixel pairs alike)
+        const int gm = (g - 1 + H) & (H - 1);
+        const size_t rm = (size_t)gm * N;
+        if constexpr (PF >= 1) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) xcur[j] = sp[ro + t + L * j];
+            for (int j = 0; j < E; ++j) xcur[j] = xnext[j];
+            if (rr < R) {
+                const size_t rn = (size_t)((g + 1) & (H - 1)) * N;
+#pragma unroll
+                for (int j = 0; j < E; ++j) xnext[j] = sp[rn + t + L * j];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < E; ++j) xcur[j] = sp[ro + t + L * j];
+        }
+        cf uy[E], fy[E], ux[E], fx[E], bb[E];
+        if constexpr (PF >= 2) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
+                if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
+            }
+            if (rr < R) {
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
+                    if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
+                }
+            }
+        }
+        if constexpr (PF >= 3) {
+            if (rr >= 1) {
+#pragma unroll
+                for (int j = 0; j < E; ++j) bb[j] = bimg[rm + t + L * j];
+            }
+        }
         RowXf<N>::c2r(xcur, buf, tw, t);
 
         // ---- y direction: a_y = x[g] - x[g-1] + u_y; z_y, u_y, w_y of row g
         cf wyc[E];
         {
-            cf uy[E], fy[E];
+            if constexpr (PF < 2) {
 #pragma unroll
-            for (int j = 0; j < E; ++j) {
-                uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
-                if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
+                for (int j = 0; j < E; ++j) {
+                    uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
+                    if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
+                }
             }
 #pragma unroll
             for (int j = 0; j < E; ++j) {
@@ -456,18 +504,19 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
 
         // ---- finalize row g-1: v = Dx^T w_x + Dy^T w_y, r = b + rho v, row FFT
         if (rr >= 1) {
-            const int gm = (g - 1 + H) & (H - 1);
-            const size_t rm = (size_t)gm * N;
             cf r[E], sh[E];
+            if constexpr (PF < 3) {
+#pragma unroll
+                for (int j = 0; j < E; ++j) bb[j] = bimg[rm + t + L * j];
+            }
 #pragma unroll
             for (int j = 0; j < E; ++j) sh[j].x = __shfl(wxp[j].x, (t + 1) & (L - 1), L);
 #pragma unroll
             for (int j = 0; j < E; ++j) {
                 const float wr = (t == L - 1) ? sh[(j + 1) & (E - 1)].x : sh[j].x;  // w_x at pixel q1+1
-                const cf bb = bimg[rm + t + L * j];
                 const float v0 = (wxp[j].x - wxp[j].y) + (wyp[j].x - wyc[j].x);
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
-                r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
+                r[j] = mkc(fmaf(rho, v0, bb[j].x), fmaf(rho, v1, bb[j].y));
             }
             RowXf<N>::r2c(r, buf, tw, t);
 #pragma unroll
@@ -476,11 +525,13 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
 
         // ---- x direction: a_x = x[g][j] - x[g][j-1] + u_x; z_x, u_x, w_x of row g
         if (rr < R) {
-            cf ux[E], fx[E], sh[E];
+            cf sh[E];
 #pragma unroll
             for (int j = 0; j < E; ++j) {
-                ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
-                if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
+                if constexpr (PF < 2) {
+                    ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
+                    if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
+                }
                 sh[j].x = __shfl(xcur[j].y, (t - 1) & (L - 1), L);
             }
 #pragma unroll

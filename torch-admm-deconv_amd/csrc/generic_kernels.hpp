@@ -1,0 +1,516 @@
+// generic_kernels.hpp -- any-size path of the ADMM-TV solver.
+//
+// The fused two-pass kernels (admm_kernels.hpp) need power-of-two H, W (register-resident
+// radix-2^k transforms).  For every other size (the reference accepts any H x W, e.g. 15 x 17)
+// the iteration runs as four simpler HIP kernels:
+//
+//   k_grow_fwd   real rows -> half spectra X[kx], kx < Wh = W/2 + 1       (rfft along W)
+//   k_gcol       per column kx: FFT along H, multiply, inverse FFT           (in place)
+//   k_grow_inv   half spectra -> real rows (Hermitian completion)          (irfft along W)
+//   k_gstep      per pixel: Dx, Dy, shrink, dual update, w, D^T w, r = b + rho v
+//
+// Transforms: LDS-resident Stockham autosort, mixed radix (4, 2, 3, 5, 7 butterflies and an
+// O(R) per-output stage for any other prime R), twiddles from the same fp64-computed
+// tables as the fast path (tw[i] = exp(-2 pi i i_/n), stored fp32).  Transforms are
+// unnormalised; 1/(H W) is folded into the multiplier tables.
+//
+// Layouts: images float [P][H][W]; spectra cf [P][H][Wh]; multipliers transposed [Wh][H]
+// (k_spectra's layout with N = W/2, so the setup kernels are shared with the fast path).
+#pragma once
+#include "admm_backward.hpp"
+
+namespace admm {
+
+constexpr int GMAXST = 24;  // max number of radix stages (n <= 8192 -> at most 13 factors)
+
+struct GPlan {
+    int n, nst;
+    int rad[GMAXST];
+};
+
+// ---------------------------------------------------------------------------
+// one Stockham stage over `lines` transforms of length n held in LDS as [i][lines]
+// (element i of line c at src[i * lines + c]); threads stride over (line, vt) pairs.
+// ---------------------------------------------------------------------------
+template <int DIR>
+__device__ __forceinline__ cf twid(const cf* __restrict__ tw, int idx) {
+    const cf w = tw[idx];
+    return DIR < 0 ? w : cconj(w);
+}
+
+template <int DIR, int R>
+__device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw, int n) {
+    if constexpr (R == 2) {
+        const cf a = v[0], b = v[1];
+        v[0] = cadd(a, b);
+        v[1] = csub(a, b);
+    } else if constexpr (R == 4) {
+        const cf t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]), t2 = cadd(v[1], v[3]);
+        const cf t3 = mul_i<DIR>(csub(v[1], v[3]));
+        v[0] = cadd(t0, t2);
+        v[2] = csub(t0, t2);
+        v[1] = cadd(t1, t3);
+        v[3] = csub(t1, t3);
+    } else {
+        // y_k = sum_q v_q W_R^{qk}, W_R^j = tw[j n / R]
+        cf y[R];
+        const int step = n / R;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            cf acc = v[0];
+#pragma unroll
+            for (int q = 1; q < R; ++q) {
+                const cf w = twid<DIR>(tw, ((q * k) % R) * step);
+                const cf p = cmul(v[q], w);
+                acc = cadd(acc, p);
+            }
+            y[k] = acc;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) v[k] = y[k];
+    }
+}
+
+template <int DIR, int R>
+__device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restrict__ dst, int n, int NS, int lines,
+                                         const cf* __restrict__ tw) {
+    const int nb = n / R;                 // butterflies per line
+    const int tstride = n / (NS * R);     // twiddle index stride of W_{NS R}
+    for (int item = threadIdx.x; item < nb * lines; item += blockDim.x) {
+        const int c = item % lines, vt = item / lines;
+        const int m = vt % NS;
+        cf v[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            cf x = src[(vt + q * nb) * lines + c];
+            if (q > 0 && m > 0) x = cmul(x, twid<DIR>(tw, m * q * tstride));
+            v[q] = x;
+        }
+        small_dft<DIR, R>(v, tw, n);
+        const int base = (vt / NS) * NS * R + m;
+#pragma unroll
+        for (int k = 0; k < R; ++k) dst[(base + k * NS) * lines + c] = v[k];
+    }
+}
+
+// any radix R: one output element per item, O(R) work
+template <int DIR>
+__device__ __forceinline__ void gstage_any(const cf* __restrict__ src, cf* __restrict__ dst, int n, int NS, int R,
+                                           int lines, const cf* __restrict__ tw) {
+    const int nb = n / R;
+    const int span = NS * R;
+    const int tstride = n / span;
+    for (int item = threadIdx.x; item < n * lines; item += blockDim.x) {
+        const int c = item % lines, o = item / lines;  // o = vt-major output slot (vt, k)
+        const int vt = o % nb, k = o / nb;
+        const int m = vt % NS;
+        const int e = m + k * NS;  // exponent base: W_{NS R}^{q (m + k NS)}
+        cf acc = src[vt * lines + c];
+        for (int q = 1; q < R; ++q) {
+            const cf w = twid<DIR>(tw, ((q * e) % span) * tstride);
+            acc = cadd(acc, cmul(src[(vt + q * nb) * lines + c], w));
+        }
+        dst[((vt / NS) * span + m + k * NS) * lines + c] = acc;
+    }
+}
+
+// full transform; data starts in bufA, returns the buffer holding the result
+template <int DIR>
+__device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf* __restrict__ tw) {
+    cf* src = bufA;
+    cf* dst = bufB;
+    int NS = 1;
+    for (int s = 0; s < pl.nst; ++s) {
+        const int R = pl.rad[s];
+        switch (R) {
+            case 2: gstage_r<DIR, 2>(src, dst, pl.n, NS, lines, tw); break;
+            case 3: gstage_r<DIR, 3>(src, dst, pl.n, NS, lines, tw); break;
+            case 4: gstage_r<DIR, 4>(src, dst, pl.n, NS, lines, tw); break;
+            case 5: gstage_r<DIR, 5>(src, dst, pl.n, NS, lines, tw); break;
+            case 7: gstage_r<DIR, 7>(src, dst, pl.n, NS, lines, tw); break;
+            default: gstage_any<DIR>(src, dst, pl.n, NS, R, lines, tw); break;
+        }
+        __syncthreads();
+        cf* t = src;
+        src = dst;
+        dst = t;
+        NS *= R;
+    }
+    return src;
+}
+
+// ---------------------------------------------------------------------------
+// row transforms: `lines` rows per block (contiguous rows of one image set)
+// ---------------------------------------------------------------------------
+struct GRowArgs {
+    const float* img;  // fwd: input rows [rows][W];   inv: output rows
+    cf* spec;          // fwd: output [rows][Wh];       inv: input
+    float* img_out;
+    const cf* tw;      // [W]
+    GPlan plan;
+    long long rows;
+    int lines;         // rows per block
+};
+
+__global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* A = tw + W;
+    cf* B = A + (size_t)W * lines;
+    for (int i = threadIdx.x; i < W; i += blockDim.x) tw[i] = a.tw[i];
+    const long long r0 = (long long)blockIdx.x * lines;
+    const int nl = (int)min((long long)lines, a.rows - r0);
+    for (int idx = threadIdx.x; idx < W * lines; idx += blockDim.x) {
+        const int c = idx / W, i = idx % W;  // coalesced along the row
+        A[i * lines + c] = mkc(c < nl ? a.img[(r0 + c) * W + i] : 0.f, 0.f);
+    }
+    __syncthreads();
+    const cf* res = gfft_lds<-1>(A, B, a.plan, lines, tw);
+    for (int idx = threadIdx.x; idx < Wh * lines; idx += blockDim.x) {
+        const int c = idx / Wh, k = idx % Wh;
+        if (c < nl) a.spec[(r0 + c) * Wh + k] = res[k * lines + c];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_grow_inv(GRowArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* A = tw + W;
+    cf* B = A + (size_t)W * lines;
+    for (int i = threadIdx.x; i < W; i += blockDim.x) tw[i] = a.tw[i];
+    const long long r0 = (long long)blockIdx.x * lines;
+    const int nl = (int)min((long long)lines, a.rows - r0);
+    for (int idx = threadIdx.x; idx < W * lines; idx += blockDim.x) {
+        const int c = idx / W, k = idx % W;
+        cf v = mkc(0.f, 0.f);
+        if (c < nl) {
+            // Hermitian completion: X[k] = conj X[W - k] for k >= Wh; the imaginary parts of
+            // the self-conjugate bins (DC, and Nyquist for even W) are dropped, as irfft does
+            if (k < Wh) {
+                v = a.spec[(r0 + c) * Wh + k];
+                if (k == 0 || 2 * k == W) v.y = 0.f;
+            } else {
+                v = cconj(a.spec[(r0 + c) * Wh + (W - k)]);
+            }
+        }
+        A[k * lines + c] = v;
+    }
+    __syncthreads();
+    const cf* res = gfft_lds<+1>(A, B, a.plan, lines, tw);
+    for (int idx = threadIdx.x; idx < W * lines; idx += blockDim.x) {
+        const int c = idx / W, i = idx % W;
+        if (c < nl) a.img_out[(r0 + c) * W + i] = res[i * lines + c].x;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// column pass: per column kx of the half spectrum, FFT along H, multiply, inverse FFT.
+// MODE 0: real factor fcT[kx][ky]; 1: mT[kx][ky]; 2: conj(mT); 3: transform only (dump the
+// forward column spectrum to `dump` and stop; used for cross-spectra).  `dump` (MODE 0) also
+// receives the forward spectrum before the multiply when non-null.
+// ---------------------------------------------------------------------------
+struct GColArgs {
+    cf* spec;        // [P][H][Wh], in place
+    cf* dump;        // optional [P][H][Wh]
+    const float* fcT;
+    const cf* mT;
+    const cf* tw;    // [H]
+    GPlan plan;      // n = H
+    int Wh;
+    int cols;        // columns per block
+    int colblocks;
+    long long P;
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* A = tw + H;
+    cf* B = A + (size_t)H * cols;
+    for (int i = threadIdx.x; i < H; i += blockDim.x) tw[i] = a.tw[i];
+    const long long p = blockIdx.x / a.colblocks;
+    const int c0 = (int)(blockIdx.x % a.colblocks) * cols;
+    const int nc = min(cols, Wh - c0);
+    cf* S = a.spec + (size_t)p * H * Wh + c0;
+    for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
+        const int i = idx / cols, c = idx % cols;  // coalesced across the block's columns
+        A[i * cols + c] = c < nc ? S[(size_t)i * Wh + c] : mkc(0.f, 0.f);
+    }
+    __syncthreads();
+    cf* res = gfft_lds<-1>(A, B, a.plan, cols, tw);
+    cf* other = (res == A) ? B : A;
+    if (a.dump) {
+        cf* D = a.dump + (size_t)p * H * Wh + c0;
+        for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
+            const int i = idx / cols, c = idx % cols;
+            if (c < nc) D[(size_t)i * Wh + c] = res[i * cols + c];
+        }
+    }
+    if constexpr (MODE == 3) return;
+    for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
+        const int ky = idx / cols, c = idx % cols;
+        if (c >= nc) continue;
+        const size_t f = (size_t)(c0 + c) * H + ky;
+        cf v = res[ky * cols + c];
+        if constexpr (MODE == 0) v = cscale(v, a.fcT[f]);
+        else if constexpr (MODE == 1) v = cmul(v, a.mT[f]);
+        else v = cmulc(v, a.mT[f]);
+        res[ky * cols + c] = v;
+    }
+    __syncthreads();
+    const cf* out = gfft_lds<+1>(res, other, a.plan, cols, tw);
+    for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
+        const int i = idx / cols, c = idx % cols;
+        if (c < nc) S[(size_t)i * Wh + c] = out[i * cols + c];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-pixel ADMM step (the generic pass A).  Thread per pixel; the w of the right and lower
+// neighbours is recomputed from the same inputs by the same expressions, so every pixel
+// sees exactly the values its neighbours compute for themselves.
+// ---------------------------------------------------------------------------
+struct GStepArgs {
+    const float* x;      // x_k                                   [P][H][W]
+    const float* b;      // H_t(xin)
+    const float* uxi;    // u_{k-1} (a_{k-1} when HIST)
+    const float* uyi;
+    float* uxo;          // u_k (a_k when HIST)
+    float* uyo;
+    float* r;            // r_{k+1} = b + rho D^T w_k (may be null: training's last iteration)
+    const float* nsq;    // iso: N_k  [2][H][W]
+    const float* nsq_prev;  // iso + HIST: N_{k-1}
+    const float* lam;
+    const float* rho;
+    int H, W;
+    long long npx;       // P H W
+};
+
+template <bool ISO, bool FIRST, bool HIST>
+__device__ __forceinline__ float gprev_u(const float* __restrict__ src, const float* __restrict__ np, size_t i, size_t hw,
+                                         float tau) {
+    if constexpr (FIRST) {
+        return 0.f;
+    } else {
+        const float v = src[i];
+        if constexpr (HIST) return v - shrink_z<ISO>(v, tau, ISO ? np[hw] : 0.f);
+        else return v;
+    }
+}
+
+template <bool ISO, bool FIRST, bool HIST>
+__global__ void __launch_bounds__(256) k_gstep(GStepArgs a) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.npx) return;
+    const int H = a.H, W = a.W;
+    const long long HW = (long long)H * W;
+    const long long pb = idx - idx % HW;
+    const int rem = (int)(idx % HW), i = rem / W, j = rem % W;
+    const int jm = j == 0 ? W - 1 : j - 1, jp = j == W - 1 ? 0 : j + 1;
+    const int im = i == 0 ? H - 1 : i - 1, ip = i == H - 1 ? 0 : i + 1;
+    const size_t P0 = (size_t)idx, PR = (size_t)(pb + (long long)i * W + jp), PD = (size_t)(pb + (long long)ip * W + j);
+    const size_t h0 = (size_t)rem, hR = (size_t)i * W + jp, hD = (size_t)ip * W + j;
+    const float rho = a.rho[0];
+    const float tau = a.lam[0] / rho;
+    const float x = a.x[P0];
+    const float xl = a.x[pb + (long long)i * W + jm], xr = a.x[PR];
+    const float xu = a.x[pb + (long long)im * W + j], xd = a.x[PD];
+    const float* npx = a.nsq_prev;
+    const float* npy = a.nsq_prev ? a.nsq_prev + HW : nullptr;
+    const float ux0 = gprev_u<ISO, FIRST, HIST>(a.uxi, npx, P0, h0, tau);
+    const float uxR = gprev_u<ISO, FIRST, HIST>(a.uxi, npx, PR, hR, tau);
+    const float uy0 = gprev_u<ISO, FIRST, HIST>(a.uyi, npy, P0, h0, tau);
+    const float uyD = gprev_u<ISO, FIRST, HIST>(a.uyi, npy, PD, hD, tau);
+    float nx0 = 0.f, nxR = 0.f, ny0 = 0.f, nyD = 0.f;
+    if constexpr (ISO) {
+        nx0 = a.nsq[h0];
+        nxR = a.nsq[hR];
+        ny0 = a.nsq[HW + h0];
+        nyD = a.nsq[HW + hD];
+    }
+    // own pixel
+    const float ax = (x - xl) + ux0, ay = (x - xu) + uy0;
+    const float zx = shrink_z<ISO>(ax, tau, nx0), zy = shrink_z<ISO>(ay, tau, ny0);
+    const float nux = ax - zx, nuy = ay - zy;
+    const float wx = zx - nux, wy = zy - nuy;
+    // right neighbour's w_x and lower neighbour's w_y
+    const float axR = (xr - x) + uxR, ayD = (xd - x) + uyD;
+    const float zxR = shrink_z<ISO>(axR, tau, nxR), zyD = shrink_z<ISO>(ayD, tau, nyD);
+    const float wxR = zxR - (axR - zxR), wyD = zyD - (ayD - zyD);
+    a.uxo[P0] = HIST ? ax : nux;
+    a.uyo[P0] = HIST ? ay : nuy;
+    if (a.r) {
+        const float v = (wx - wxR) + (wy - wyD);
+        a.r[P0] = fmaf(rho, v, a.b[P0]);
+    }
+}
+
+// iso: N_k[pixel] = sum over planes of a_x^2, a_y^2 with a = D x_k + u_{k-1}
+template <bool FIRST, bool HIST>
+__global__ void __launch_bounds__(256) k_giso_norm(const float* __restrict__ x, const float* __restrict__ uxi,
+                                                   const float* __restrict__ uyi, const float* __restrict__ nprev,
+                                                   const float* __restrict__ lam, const float* __restrict__ rho,
+                                                   float* __restrict__ nsq, int H, int W, long long P) {
+    const long long HW = (long long)H * W;
+    const long long hw = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (hw >= HW) return;
+    const int i = (int)(hw / W), j = (int)(hw % W);
+    const int jm = j == 0 ? W - 1 : j - 1, im = i == 0 ? H - 1 : i - 1;
+    const float tau = lam[0] / rho[0];
+    float sx = 0.f, sy = 0.f;
+    for (long long p = 0; p < P; ++p) {
+        const long long o = p * HW;
+        const float xc = x[o + hw];
+        const float ux = gprev_u<true, FIRST, HIST>(uxi, nprev, (size_t)(o + hw), (size_t)hw, tau);
+        const float uy = gprev_u<true, FIRST, HIST>(uyi, nprev ? nprev + HW : nullptr, (size_t)(o + hw), (size_t)hw, tau);
+        const float ax = (xc - x[o + (long long)i * W + jm]) + ux;
+        const float ay = (xc - x[o + (long long)im * W + j]) + uy;
+        sx = fmaf(ax, ax, sx);
+        sy = fmaf(ay, ay, sy);
+    }
+    nsq[hw] = sx;
+    nsq[HW + hw] = sy;
+}
+
+// ---------------------------------------------------------------------------
+// backward: per-pixel reverse step (the generic k_bwd_pass_a)
+// ---------------------------------------------------------------------------
+struct GBwdArgs {
+    const float* rb;      // r^_k                               [P][H][W]
+    float* xb;            // x^_{k-1} (k >= 2)
+    float* bbar;          // b^ accumulator
+    const float* abx_in;  // a^_k (k < K)
+    const float* aby_in;
+    float* abx_out;       // a^_{k-1} (k >= 2)
+    float* aby_out;
+    const float* akx;     // a_k
+    const float* aky;
+    const float* apx;     // a_{k-1} (k >= 2)
+    const float* apy;
+    const float* np;      // iso: N_{k-1}  [2][H][W]
+    const float* qp;      // iso: Q_{k-1}  [2][H][W]
+    const float* lam;
+    const float* rho;
+    float* part;          // per block {rho^, tau^}
+    int H, W;
+    long long npx;
+};
+
+template <bool ISO, bool LASTK, bool FIRSTK>
+__device__ __forceinline__ float gabar(float d, float ap, float ub, float tau, float rho, float n, float q) {
+    const float wb = rho * d;
+    const float zb = 2.f * wb - ub;
+    return ub - wb + shrink_vjp<ISO>(ap, zb, tau, n, q);
+}
+
+template <bool ISO, bool LASTK, bool FIRSTK>
+__global__ void __launch_bounds__(256) k_gbwd(GBwdArgs a) {
+    __shared__ float red[2][256];
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    float rho_acc = 0.f, tau_acc = 0.f;
+    if (idx < a.npx) {
+        const int H = a.H, W = a.W;
+        const long long HW = (long long)H * W;
+        const long long pb = idx - idx % HW;
+        const int rem = (int)(idx % HW), i = rem / W, j = rem % W;
+        const int jm = j == 0 ? W - 1 : j - 1, jp = j == W - 1 ? 0 : j + 1;
+        const int im = i == 0 ? H - 1 : i - 1, ip = i == H - 1 ? 0 : i + 1;
+        const size_t P0 = (size_t)idx, PR = (size_t)(pb + (long long)i * W + jp), PD = (size_t)(pb + (long long)ip * W + j);
+        const size_t h0 = (size_t)rem, hR = (size_t)i * W + jp, hD = (size_t)ip * W + j;
+        const float rho = a.rho[0];
+        const float tau = a.lam[0] / rho;
+        const float r0 = a.rb[P0];
+        const float rl = a.rb[pb + (long long)i * W + jm], rr = a.rb[PR];
+        const float ru = a.rb[pb + (long long)im * W + j], rd = a.rb[PD];
+        const float dx0 = r0 - rl, dy0 = r0 - ru;  // D r^ at the pixel
+        // rho^ partial: D r^ . (w_{k-1} - D x_k), w = 2z - a, D x_k = a_k - a_{k-1} + z_{k-1}
+        float apx0 = 0.f, apy0 = 0.f, nx0 = 0.f, ny0 = 0.f;
+        if constexpr (!FIRSTK) {
+            apx0 = a.apx[P0];
+            apy0 = a.apy[P0];
+            if constexpr (ISO) {
+                nx0 = a.np[h0];
+                ny0 = a.np[HW + h0];
+            }
+        }
+        const float zpx = FIRSTK ? 0.f : shrink_z<ISO>(apx0, tau, nx0);
+        const float zpy = FIRSTK ? 0.f : shrink_z<ISO>(apy0, tau, ny0);
+        {
+            const float ex = (2.f * zpx - apx0) - (a.akx[P0] - apx0 + zpx);
+            const float ey = (2.f * zpy - apy0) - (a.aky[P0] - apy0 + zpy);
+            rho_acc = fmaf(dx0, ex, dy0 * ey);
+        }
+        // b^ += r^
+        a.bbar[P0] = LASTK ? r0 : a.bbar[P0] + r0;
+        if constexpr (!FIRSTK) {
+            float qx0 = 0.f, qy0 = 0.f, qxR = 0.f, qyD = 0.f, nxR = 0.f, nyD = 0.f;
+            if constexpr (ISO) {
+                qx0 = a.qp[h0];
+                qy0 = a.qp[HW + h0];
+                qxR = a.qp[hR];
+                qyD = a.qp[HW + hD];
+                nxR = a.np[hR];
+                nyD = a.np[HW + hD];
+            }
+            const float ubx0 = LASTK ? 0.f : a.abx_in[P0], uby0 = LASTK ? 0.f : a.aby_in[P0];
+            const float ubxR = LASTK ? 0.f : a.abx_in[PR], ubyD = LASTK ? 0.f : a.aby_in[PD];
+            const float abx0 = gabar<ISO, LASTK, FIRSTK>(dx0, apx0, ubx0, tau, rho, nx0, qx0);
+            const float aby0 = gabar<ISO, LASTK, FIRSTK>(dy0, apy0, uby0, tau, rho, ny0, qy0);
+            // a^_x at the right neighbour, a^_y at the lower one
+            const float abxR = gabar<ISO, LASTK, FIRSTK>(rr - r0, a.apx[PR], ubxR, tau, rho, nxR, qxR);
+            const float abyD = gabar<ISO, LASTK, FIRSTK>(rd - r0, a.apy[PD], ubyD, tau, rho, nyD, qyD);
+            a.abx_out[P0] = abx0;
+            a.aby_out[P0] = aby0;
+            a.xb[P0] = (abx0 - abxR) + (aby0 - abyD);
+            if constexpr (!ISO) {
+                const float wbx = rho * dx0, wby = rho * dy0;
+                tau_acc = soft_dtau(apx0, 2.f * wbx - ubx0, tau) + soft_dtau(apy0, 2.f * wby - uby0, tau);
+            }
+        }
+    }
+    red[0][threadIdx.x] = rho_acc;
+    red[1][threadIdx.x] = tau_acc;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + o];
+            red[1][threadIdx.x] += red[1][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        a.part[2 * blockIdx.x + 0] = red[0][0];
+        a.part[2 * blockIdx.x + 1] = red[1][0];
+    }
+}
+
+// iso backward: Q_{k-1}[pixel] = sum over planes of a_{k-1} z^_{k-1}, z^ = 2 rho D r^_k - a^_k
+template <bool LASTK>
+__global__ void __launch_bounds__(256) k_giso_q(const float* __restrict__ rb, const float* __restrict__ abx,
+                                                const float* __restrict__ aby, const float* __restrict__ apx,
+                                                const float* __restrict__ apy, const float* __restrict__ rho_p,
+                                                float* __restrict__ q, int H, int W, long long P) {
+    const long long HW = (long long)H * W;
+    const long long hw = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (hw >= HW) return;
+    const int i = (int)(hw / W), j = (int)(hw % W);
+    const int jm = j == 0 ? W - 1 : j - 1, im = i == 0 ? H - 1 : i - 1;
+    const float rho = rho_p[0];
+    float qx = 0.f, qy = 0.f;
+    for (long long p = 0; p < P; ++p) {
+        const long long o = p * HW;
+        const float r0 = rb[o + hw];
+        const float zx = 2.f * rho * (r0 - rb[o + (long long)i * W + jm]) - (LASTK ? 0.f : abx[o + hw]);
+        const float zy = 2.f * rho * (r0 - rb[o + (long long)im * W + j]) - (LASTK ? 0.f : aby[o + hw]);
+        qx = fmaf(apx[o + hw], zx, qx);
+        qy = fmaf(apy[o + hw], zy, qy);
+    }
+    q[hw] = qx;
+    q[HW + hw] = qy;
+}
+
+}  // namespace admm
