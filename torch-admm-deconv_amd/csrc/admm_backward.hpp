@@ -516,10 +516,12 @@ __global__ void k_xspec_reduce(const cf* __restrict__ part, int ngroups, long lo
 }
 
 // kbar[a][b] (one block per tap) from A (fc^2-weighted, scaled sums), Z (scaled) and sigma.
-// Scalings: row spectra carry a factor 2, fc is stored / (2HW):
-//   A_true = (HW)^2 A,  Z_true = Z / 4.
+// Scalings: fast path -- row spectra carry a factor 2, fc is stored / (2HW):
+//   A_true = (HW)^2 A,  Z_true = Z / 4  (zscale 0.25);
+// generic path -- plain rfft spectra, fc stored / (HW): A_true = (HW)^2 A, Z_true = Z (zscale 1).
 __global__ void k_psf_grad(const double2* __restrict__ A, const double2* __restrict__ Z,
-                           const double2* __restrict__ sigma, int k, int H, int W, float* __restrict__ gk) {
+                           const double2* __restrict__ sigma, int k, int H, int W, float* __restrict__ gk,
+                           double zscale) {
     __shared__ double red[256];
     const int tap = blockIdx.x;
     const int a = tap / k, b = tap % k, c = k / 2;
@@ -529,7 +531,7 @@ __global__ void k_psf_grad(const double2* __restrict__ A, const double2* __restr
     double acc = 0.0;
     for (long long i = threadIdx.x; i < nf; i += blockDim.x) {
         const int kx = (int)(i / H), ky = (int)(i % H);
-        const double cw = (kx == 0 || kx == N) ? 1.0 : 2.0;
+        const double cw = (kx == 0 || 2 * kx == W) ? 1.0 : 2.0;  // self-conjugate columns once
         double s, co;
         // through fc: dL/ds2 * 2 Re(conj(sigma) e^{-2 pi i (a ky/H + b kx/W)})
         const long long ph2 = ((long long)a * ky % H) * W + ((long long)b * kx % W) * H;  // units 1/(HW)
@@ -545,7 +547,7 @@ __global__ void k_psf_grad(const double2* __restrict__ A, const double2* __restr
         const long long p1 = (ph1 * W + ph1x * H) % (long long)HW;
         sincospi(2.0 * (double)p1 / HW, &s, &co);
         const double2 z = Z[i];
-        acc += cw / HW * 0.25 * (z.x * co + z.y * s);  // Re((zx + i zy)(co - i s))
+        acc += cw / HW * zscale * (z.x * co + z.y * s);  // Re((zx + i zy)(co - i s))
     }
     red[threadIdx.x] = acc;
     __syncthreads();

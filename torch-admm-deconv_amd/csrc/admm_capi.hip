@@ -347,8 +347,6 @@ int validate(const admm_tv_desc* d) {
     if (!supported_hw(d->H, d->W) && !generic_hw(d->H, d->W))
         return fail(ADMM_TV_EUNSUPPORTED, "H and W must be in [1, 4096]");
     if (d->kh > d->H || d->kw > d->W) return fail(ADMM_TV_EKERNEL, "PSF larger than the image");
-    if (generic_hw(d->H, d->W) && d->kh > 0 && (d->flags & ADMM_TV_FLAG_PSF_GRAD))
-        return fail(ADMM_TV_EUNSUPPORTED, "PSF gradient needs power-of-two H, W in this build");
     return 0;
 }
 
@@ -523,6 +521,7 @@ int gbwd(const GBwdArgs& a, bool iso, bool lastk, bool firstk, hipStream_t s) {
 // history (training) storage: a_k for k = 1..K (x and y images), iso norms N_k
 struct Hist {
     size_t a_slot;     // bytes of one image
+    size_t t_slot;     // bytes of one kept spectrum (fast path: row spectra; generic: 2-D half spectra)
     size_t n_slot;     // bytes of one norm pair [2][H][W]
     size_t n_off;      // offset of the norm history
     size_t t_off;      // offset of the r_k spectra (PSF gradient only)
@@ -537,7 +536,8 @@ Hist make_hist(const admm_tv_desc& d) {
     h.n_off = (size_t)d.maxit * 2 * h.a_slot;
     h.t_off = h.n_off + (size_t)d.maxit * h.n_slot;
     h.keep_t = d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD);
-    h.total = h.t_off + (h.keep_t ? (size_t)d.maxit * h.a_slot : 0);
+    h.t_slot = generic_hw(d.H, d.W) ? up((size_t)d.B * d.C * d.H * (d.W / 2 + 1) * sizeof(cf)) : h.a_slot;
+    h.total = h.t_off + (h.keep_t ? (size_t)d.maxit * h.t_slot : 0);
     return h;
 }
 
@@ -564,6 +564,10 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, c
     auto hn = [&](int k) -> float* {
         return reinterpret_cast<float*>(static_cast<char*>(hist) + Hs.n_off + (size_t)(k - 1) * Hs.n_slot);
     };
+    const bool keep_t = train && Hs.keep_t;  // PSF gradient: keep every r_k's 2-D spectrum
+    auto ht = [&](int k) -> cf* {
+        return reinterpret_cast<cf*>(static_cast<char*>(hist) + Hs.t_off + (size_t)(k - 1) * Hs.t_slot);
+    };
     const float* bimg = xin;
     if (d.kh > 0) {  // b = H_t(xin) once
         ProfScope ps(3, s);
@@ -580,7 +584,7 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, c
         const bool last = it == d.maxit;
         {
             ProfScope ps(1, s);
-            if (int e = gcol(spec, nullptr, fcT, mT, twH, H, W, P, 0, s)) return e;
+            if (int e = gcol(spec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, P, 0, s)) return e;
             if (int e = grow_inv(spec, last ? out : ximg, twW, W, rows, s)) return e;
         }
         if (last && !train) break;
@@ -662,7 +666,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     };
     const bool keep_t = train && Hs.keep_t;
     auto ht = [&](int k) -> cf* {  // r_k row spectra (k >= 1), kept for the PSF gradient
-        return reinterpret_cast<cf*>(static_cast<char*>(hist) + Hs.t_off + (size_t)(k - 1) * Hs.a_slot);
+        return reinterpret_cast<cf*>(static_cast<char*>(hist) + Hs.t_off + (size_t)(k - 1) * Hs.t_slot);
     };
 
     // b = H_t(xin) once (the reference recomputes it every iteration, deconv.py:104)
@@ -774,7 +778,8 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
         const size_t nf = ((size_t)d.W / 2 + 1) * d.H;
         B.xppg = 8;
         B.xgroups = (int)((d.B * d.C + B.xppg - 1) / B.xppg);
-        B.xpart = take((size_t)B.xgroups * nf * sizeof(cf));
+        // fast path: per-plane-group cross-spectrum partials; generic: one 2-D spectrum set
+        B.xpart = take((B.f.gen ? (size_t)d.B * d.C : (size_t)B.xgroups) * nf * sizeof(cf));
         B.aacc = take(nf * sizeof(double2));
         B.zacc = take(nf * sizeof(double2));
     }
@@ -784,8 +789,9 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
 
 
 // generic-size backward (same contract as admm_tv_backward, PSF gradient excluded)
-int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* lam, const float* rho, const float* gout,
-                     const void* hist, float* gxin, float* glam, float* grho, void* ws, hipStream_t s) {
+int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xin, const float* lam, const float* rho,
+                     const float* gout, const void* hist, float* gxin, float* glam, float* grho, float* gkern, void* ws,
+                     hipStream_t s) {
     const Layout& Lo = BL.f;
     const long long P = d.B * d.C;
     const int H = (int)d.H, W = (int)d.W, K = d.maxit;
@@ -797,6 +803,20 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* la
         return reinterpret_cast<const float*>(hb + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
     };
     auto hn = [&](int k) -> const float* { return reinterpret_cast<const float*>(hb + Hs.n_off + (size_t)(k - 1) * Hs.n_slot); };
+    auto ht = [&](int k) -> const cf* { return reinterpret_cast<const cf*>(hb + Hs.t_off + (size_t)(k - 1) * Hs.t_slot); };
+    const bool psf_grad = gkern != nullptr;
+    const int Wh = W / 2 + 1;
+    const long long nf = (long long)Wh * H;
+    cf* xspec = psf_grad ? at<cf>(ws, BL.xpart) : nullptr;  // 2-D spectra of x^_k (then of b^)
+    if (psf_grad) {
+        HIPCHK(hipMemsetAsync(at<double2>(ws, BL.aacc), 0, nf * sizeof(double2), s));
+        HIPCHK(hipMemsetAsync(at<double2>(ws, BL.zacc), 0, nf * sizeof(double2), s));
+    }
+    cf* twW = at<cf>(ws, Lo.twW);
+    cf* twH = at<cf>(ws, Lo.twH);
+    float* fcT = at<float>(ws, Lo.fcT);
+    const long long rows = P * H;
+    const dim3 fgrid((unsigned)((nf + 255) / 256)), fblk(256);
     cf* spec = at<cf>(ws, Lo.spec[0]);
     float* rb = at<float>(ws, Lo.spec[1]);   // r^_k
     float* xbuf[2] = {at<float>(ws, Lo.rimg), at<float>(ws, Lo.u[0])};  // x^ ping-pong
@@ -813,7 +833,15 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* la
         const bool lastk = (k == K), firstk = (k == 1);
         {
             ProfScope ps(1, s);
-            if (int e = gapply(xbk, rb, spec, Lo, ws, d, 0, s)) return e;  // r^_k = M x^_k
+            // r^_k = M x^_k; with the PSF gradient the column pass also dumps X^_k's spectrum and
+            // A += fc^2 Re(sum_p conj(X^_k) R_k)
+            if (int e = grow_fwd(xbk, spec, twW, W, rows, s)) return e;
+            if (int e = gcol(spec, xspec, fcT, at<cf>(ws, Lo.mT), twH, H, W, P, 0, s)) return e;
+            if (int e = grow_inv(spec, rb, twW, W, rows, s)) return e;
+            if (psf_grad) {
+                hipLaunchKernelGGL(k_gxspec_acc, fgrid, fblk, 0, s, xspec, ht(k), P, H, Wh, fcT, at<double2>(ws, BL.aacc));
+                if (int e = launch_check("k_gxspec_acc")) return e;
+            }
         }
         if (d.iso && !firstk) {
             ProfScope ps(2, s);
@@ -850,6 +878,17 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* la
         if (int e = launch_check("k_bwd_scalars")) return e;
     } else if (glam || grho) {
         return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
+    }
+    if (psf_grad) {  // Z = sum_p conj(Bbar_p) Xin_p, then the k x k taps
+        if (int e = grow_fwd(bbar, spec, twW, W, rows, s)) return e;
+        if (int e = gcol(spec, xspec, nullptr, nullptr, twH, H, W, P, 3, s)) return e;
+        if (int e = grow_fwd(xin, spec, twW, W, rows, s)) return e;
+        if (int e = gcol(spec, spec, nullptr, nullptr, twH, H, W, P, 3, s)) return e;
+        hipLaunchKernelGGL(k_gxspec_acc, fgrid, fblk, 0, s, xspec, spec, P, H, Wh, nullptr, at<double2>(ws, BL.zacc));
+        if (int e = launch_check("k_gxspec_acc")) return e;
+        hipLaunchKernelGGL(k_psf_grad, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
+                           at<double2>(ws, BL.zacc), at<double2>(ws, Lo.sigma), d.kh, H, W, gkern, 1.0);
+        if (int e = launch_check("k_psf_grad")) return e;
     }
     if (gxin && d.kh > 0)  // x^_in = H_t^T b^
         if (int e = gapply(bbar, gxin, spec, Lo, ws, d, 2, s)) return e;
@@ -932,17 +971,14 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     }
     if (!hist || hist_bytes < make_hist(d).total) return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
-    if (Lo.gen) {
-        if (psf_grad) return fail(ADMM_TV_EUNSUPPORTED, "PSF gradient needs power-of-two H, W in this build");
-        return run_backward_gen(d, BL, lam, rho, gout, hist, gxin, glam, grho, ws, s);
-    }
+    if (Lo.gen) return run_backward_gen(d, BL, xin, lam, rho, gout, hist, gxin, glam, grho, gkern, ws, s);
     const Hist Hs = make_hist(d);
     char* hb = static_cast<char*>(const_cast<void*>(hist));
     auto ha = [&](int k, int comp) -> const float* {
         return reinterpret_cast<const float*>(hb + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
     };
     auto hn = [&](int k) -> const float* { return reinterpret_cast<const float*>(hb + Hs.n_off + (size_t)(k - 1) * Hs.n_slot); };
-    auto ht = [&](int k) -> const cf* { return reinterpret_cast<const cf*>(hb + Hs.t_off + (size_t)(k - 1) * Hs.a_slot); };
+    auto ht = [&](int k) -> const cf* { return reinterpret_cast<const cf*>(hb + Hs.t_off + (size_t)(k - 1) * Hs.t_slot); };
     const long long nf = (long long)(N + 1) * H;
     if (psf_grad) {
         HIPCHK(hipMemsetAsync(at<double2>(ws, BL.aacc), 0, nf * sizeof(double2), s));
@@ -1022,7 +1058,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
                            BL.xgroups, nf, nullptr, at<double2>(ws, BL.zacc));
         if ((e = launch_check("k_xspec_reduce"))) return e;
         hipLaunchKernelGGL(k_psf_grad, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
-                           at<double2>(ws, BL.zacc), at<double2>(ws, Lo.sigma), d.kh, H, W, gkern);
+                           at<double2>(ws, BL.zacc), at<double2>(ws, Lo.sigma), d.kh, H, W, gkern, 0.25);
         if ((e = launch_check("k_psf_grad"))) return e;
     }
     if (gxin && d.kh > 0) {

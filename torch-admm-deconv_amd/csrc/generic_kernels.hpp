@@ -513,4 +513,29 @@ __global__ void __launch_bounds__(256) k_giso_q(const float* __restrict__ rb, co
     q[HW + hw] = qy;
 }
 
+// PSF gradient on the generic path: acc[kx][ky] += sum_p conj(U_p) V_p at every half-plane
+// frequency, U, V 2-D spectra [P][H][Wh] (column-pass dumps).  With fcT: only
+// fc^2 Re(conj(U) V) is kept (the Wiener-factor path); without: the complex sum (Z).
+__global__ void k_gxspec_acc(const cf* __restrict__ U, const cf* __restrict__ V, long long P, int H, int Wh,
+                             const float* __restrict__ fcT, double2* __restrict__ acc) {
+    const long long nf = (long long)H * Wh;
+    const long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nf) return;
+    const int ky = (int)(f / Wh), kx = (int)(f % Wh);
+    double re = 0.0, im = 0.0;
+    for (long long p = 0; p < P; ++p) {
+        const cf u = U[p * nf + f], v = V[p * nf + f];
+        re += (double)u.x * v.x + (double)u.y * v.y;
+        im += (double)u.x * v.y - (double)u.y * v.x;
+    }
+    const size_t i = (size_t)kx * H + ky;
+    if (fcT) {
+        const double c = fcT[i];
+        acc[i].x += c * c * re;
+    } else {
+        acc[i].x += re;
+        acc[i].y += im;
+    }
+}
+
 }  // namespace admm
