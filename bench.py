@@ -35,6 +35,8 @@ CONFIGS = {
     # name: (B, C, H, W, psf kind, k, maxit, iso, description)
     "c3": (64, 3, 1024, 1024, "gauss:3", 21, 50, False,
            "C3/metric: batch-64 1024x1024x3, 21x21 Gaussian PSF (sigma 3), lambda 0.01, rho 0.02, aniso, 50 iters"),
+    "c3x100": (64, 3, 1024, 1024, "gauss:3", 21, 100, False,
+               "C3 at 100 iters (SURVEY §8 d1): batch-64 1024x1024x3, 21x21 Gaussian PSF, aniso"),
     "c2": (32, 3, 512, 512, "motion", 15, 50, False,
            "C2: batch-32 512x512x3, 15x15 motion PSF, lambda 0.01, rho 0.02, aniso, 50 iters"),
     "c5fwd": (16, 3, 512, 512, "none", 0, 100, True,
@@ -73,7 +75,7 @@ def pmc_traffic(config: str, kernel: str, launches: int, steps: int):
     (profiles/*_pmc_summary.json, made by tools/pmc/run_pmc.sh + summarize.py: separate
     FETCH_SIZE / WRITE_SIZE passes, gfx950 corrections calibrated on the box).  None if absent."""
     import glob
-    if config != "c3":
+    if config not in ("c3", "c3x100"):
         return None, None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not files:
