@@ -7,3 +7,8 @@ Public surface (same import paths as the reference):
 The solver runs as hand-written HIP kernels through the C ABI in include/admm_tv.h.
 """
 __version__ = "0.1.0"
+
+# Overlay: when the reference tree is also on sys.path (after this package), its modules that
+# this build does not provide (training loop, metrics, data loading, other models) stay
+# importable under the same package name; modules present here take precedence.
+__path__ = __import__("pkgutil").extend_path(__path__, __name__)

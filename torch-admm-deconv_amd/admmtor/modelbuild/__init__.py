@@ -1,2 +1,7 @@
-"""admmtor.modelbuild -- only the pieces of the reference's modelbuild that act on ADMMDeconv
-(the parameter clamps).  The CNN models themselves are not part of this build."""
+"""admmtor.modelbuild -- the config-5 caller (DivergentRestorer, DivergentAttention and their blocks)
+and the ADMMDeconv parameter clamps, mirroring the reference's modelbuild."""
+
+# Overlay: when the reference tree is also on sys.path (after this package), its modules that
+# this build does not provide (training loop, metrics, data loading, other models) stay
+# importable under the same package name; modules present here take precedence.
+__path__ = __import__("pkgutil").extend_path(__path__, __name__)
