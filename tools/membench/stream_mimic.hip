@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <cstdlib>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
@@ -45,6 +46,160 @@ __global__ void __launch_bounds__(256) k_mimic(const cf* __restrict__ sp, const 
         }
         if (rr < R) {
             for (int j = 0; j < E; ++j) { cf u = uxi[ro + t + L * j]; u.x -= x[j].y; u.y += x[j].x; st(&uxo[ro + t + L * j], u, NT); }
+        }
+        for (int j = 0; j < E; ++j) acc[j] = x[j];
+    }
+}
+
+// strip-walking with only 1 read + 1 write stream (isolates the walk from the stream count)
+template <int R>
+__global__ void __launch_bounds__(256) k_walk11(const cf* __restrict__ sp, cf* __restrict__ so, int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    for (int rr = 0; rr < R; ++rr) {
+        const size_t ro = base + (size_t)(i0 + rr) * N;
+        cf x[E];
+        for (int j = 0; j < E; ++j) x[j] = sp[ro + t + L * j];
+        for (int j = 0; j < E; ++j) { x[j].x *= 1.0001f; so[ro + t + L * j] = x[j]; }
+    }
+}
+
+// walk variants: MODE 0 contiguous strips (pass A's mapping), 1 row-interleaved (wave w takes
+// rows w, w + S, w + 2S ... so concurrent waves touch adjacent rows), 2 consecutive waves in
+// different planes
+template <int R, int MODE>
+__global__ void __launch_bounds__(256) k_walkv(const cf* __restrict__ sp, cf* __restrict__ so, int H, long long nstrips,
+                                               int P) {
+    const int t = threadIdx.x % L;
+    const long long w = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (w >= nstrips) return;
+    for (int rr = 0; rr < R; ++rr) {
+        size_t ro;
+        if (MODE == 0) {
+            ro = (size_t)(w * R + rr) * N;
+        } else if (MODE == 1) {
+            ro = (size_t)(rr * nstrips + w) * N;
+        } else {
+            const long long spp = H / R;
+            const long long p = w % P, s = w / P;
+            ro = ((size_t)p * H + s * R + rr) * N;
+        }
+        cf x[E];
+        for (int j = 0; j < E; ++j) x[j] = sp[ro + t + L * j];
+        for (int j = 0; j < E; ++j) { x[j].x *= 1.0001f; so[ro + t + L * j] = x[j]; }
+    }
+}
+
+// 4R+3W, two rows per step (twice the bytes in flight per wave)
+template <int R>
+__global__ void __launch_bounds__(256) k_mimic2(const cf* __restrict__ sp, const cf* __restrict__ uxi,
+                                                const cf* __restrict__ uyi, const cf* __restrict__ b,
+                                                cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
+                                                int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    for (int rr = 0; rr < R; rr += 2) {
+        const size_t r0 = base + (size_t)(i0 + rr) * N, r1 = r0 + N;
+        cf x0[E], x1[E], a0[E], a1[E], c0[E], c1[E], d0[E], d1[E];
+        for (int j = 0; j < E; ++j) { x0[j] = sp[r0 + t + L * j]; x1[j] = sp[r1 + t + L * j]; }
+        for (int j = 0; j < E; ++j) { a0[j] = uxi[r0 + t + L * j]; a1[j] = uxi[r1 + t + L * j]; }
+        for (int j = 0; j < E; ++j) { c0[j] = uyi[r0 + t + L * j]; c1[j] = uyi[r1 + t + L * j]; }
+        for (int j = 0; j < E; ++j) { d0[j] = b[r0 + t + L * j]; d1[j] = b[r1 + t + L * j]; }
+        for (int j = 0; j < E; ++j) {
+            uxo[r0 + t + L * j] = make_float2(a0[j].x + x0[j].x, a0[j].y); uxo[r1 + t + L * j] = make_float2(a1[j].x + x1[j].x, a1[j].y);
+            uyo[r0 + t + L * j] = make_float2(c0[j].x - x0[j].y, c0[j].y); uyo[r1 + t + L * j] = make_float2(c1[j].x - x1[j].y, c1[j].y);
+            so[r0 + t + L * j] = make_float2(d0[j].x * x0[j].x, d0[j].y); so[r1 + t + L * j] = make_float2(d1[j].x * x1[j].x, d1[j].y);
+        }
+    }
+}
+
+// pass A's 4R+3W walk over a row-permuted layout: logical row i of a plane is stored at
+// position (i % R) * (H / R) + i / R, so at each step the waves of one plane touch adjacent rows
+template <int R>
+__global__ void __launch_bounds__(256) k_mimic_perm(const cf* __restrict__ sp, const cf* __restrict__ uxi,
+                                                    const cf* __restrict__ uyi, const cf* __restrict__ b,
+                                                    cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
+                                                    int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    auto prow = [&](int i) { i &= (H - 1); return (size_t)((i % R) * spp + i / R) * N; };
+    cf acc[E];
+    for (int j = 0; j < E; ++j) acc[j] = sp[base + prow(i0 - 1) + t + L * j];
+    for (int rr = 0; rr <= R; ++rr) {
+        const size_t ro = base + prow(i0 + rr);
+        const size_t rm = base + prow(i0 + rr - 1);
+        cf x[E], uy[E];
+        for (int j = 0; j < E; ++j) x[j] = sp[ro + t + L * j];
+        for (int j = 0; j < E; ++j) { uy[j] = uyi[ro + t + L * j]; uy[j].x += x[j].x; uy[j].y += acc[j].y; }
+        if (rr < R) for (int j = 0; j < E; ++j) uyo[ro + t + L * j] = uy[j];
+        if (rr >= 1) {
+            for (int j = 0; j < E; ++j) { cf bb = b[rm + t + L * j]; acc[j].x += bb.x; acc[j].y -= bb.y; }
+            for (int j = 0; j < E; ++j) so[rm + t + L * j] = acc[j];
+        }
+        if (rr < R) {
+            for (int j = 0; j < E; ++j) { cf u = uxi[ro + t + L * j]; u.x -= x[j].y; u.y += x[j].x; uxo[ro + t + L * j] = u; }
+        }
+        for (int j = 0; j < E; ++j) acc[j] = x[j];
+    }
+}
+
+// pass B's access over the permuted layout: column block, logical row r at stored row perm(r)
+template <int C, int TPB, int R>
+__global__ void __launch_bounds__(TPB) k_colmimic_perm(cf* __restrict__ spec, int H, int colblocks) {
+    constexpr int L = TPB / C;
+    const int c = threadIdx.x % C, t = threadIdx.x / C;
+    const int p = blockIdx.x / colblocks, cb = blockIdx.x % colblocks;
+    cf* base = spec + (size_t)p * H * N + cb * C + c;
+    const int E = H / L, spp = H / R;
+    cf v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < E) { const int r = t + L * j; v[j] = base[(size_t)((r % R) * spp + r / R) * N]; }
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < E) { const int r = t + L * j; v[j].x *= 1.0001f; base[(size_t)((r % R) * spp + r / R) * N] = v[j]; }
+}
+
+// row records: per row {spectrum, u_x, u_y} contiguous (3N cf), ping-pong in/out; b separate
+template <int R>
+__global__ void __launch_bounds__(256) k_mimic_rec(const cf* __restrict__ ri, const cf* __restrict__ b,
+                                                   cf* __restrict__ ro_, int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    auto rec = [&](int i) { return 3 * (base + (size_t)(i & (H - 1)) * N); };
+    cf acc[E];
+    for (int j = 0; j < E; ++j) acc[j] = ri[rec(i0 - 1) + t + L * j];
+    for (int rr = 0; rr <= R; ++rr) {
+        const size_t r0 = rec(i0 + rr), rm = rec(i0 + rr - 1);
+        cf x[E], uy[E];
+        for (int j = 0; j < E; ++j) x[j] = ri[r0 + t + L * j];
+        for (int j = 0; j < E; ++j) { uy[j] = ri[r0 + 2 * N + t + L * j]; uy[j].x += x[j].x; uy[j].y += acc[j].y; }
+        if (rr < R) for (int j = 0; j < E; ++j) ro_[r0 + 2 * N + t + L * j] = uy[j];
+        if (rr >= 1) {
+            const size_t bm = base + (size_t)((i0 + rr - 1) & (H - 1)) * N;
+            for (int j = 0; j < E; ++j) { cf bb = b[bm + t + L * j]; acc[j].x += bb.x; acc[j].y -= bb.y; }
+            for (int j = 0; j < E; ++j) ro_[rm + t + L * j] = acc[j];
+        }
+        if (rr < R) {
+            for (int j = 0; j < E; ++j) { cf u = ri[r0 + N + t + L * j]; u.x -= x[j].y; u.y += x[j].x; ro_[r0 + N + t + L * j] = u; }
         }
         for (int j = 0; j < E; ++j) acc[j] = x[j];
     }
@@ -122,6 +277,9 @@ int main() {
     cf *ui, *uo;
     CK(hipMalloc(&ui, 2 * n * sizeof(cf))); CK(hipMalloc(&uo, 2 * n * sizeof(cf)));
     CK(hipMemset(ui, 0, 2 * n * sizeof(cf)));
+    cf *reci, *reco;
+    CK(hipMalloc(&reci, 3 * n * sizeof(cf))); CK(hipMalloc(&reco, 3 * n * sizeof(cf)));
+    CK(hipMemset(reci, 0, 3 * n * sizeof(cf)));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     auto timeit = [&](const char* name, double bytes, auto launch) {
@@ -136,6 +294,16 @@ int main() {
         printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
     const double arr = (double)n * sizeof(cf);
+    if (getenv("AB_ONLY")) {
+        const long long ns = (long long)P * H / 8;
+        for (int rep = 0; rep < 4; ++rep) {
+            timeit("A  separate u 4R+3W R=8", 7 * arr, [&] { k_mimic<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("B  interleaved u 3R+2W R=8", 7 * arr, [&] { k_mimic_il<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], ui, buf[3], uo, buf[6], H, ns); });
+            timeit("C  row records 2R+1W R=8", 7 * arr, [&] { k_mimic_rec<8><<<(unsigned)((ns + 3) / 4), 256>>>(reci, buf[3], reco, H, ns); });
+            timeit("D  interleaved u R=4", 7 * arr, [&] { k_mimic_il<4><<<(unsigned)((2 * ns + 3) / 4), 256>>>(buf[0], ui, buf[3], uo, buf[6], H, 2 * ns); });
+        }
+        return 0;
+    }
     timeit("copy 1R+1W (float4, grid-stride 4096 blk)", 2 * arr, [&] { k_copy<false><<<4096, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
     timeit("copy nt-store (float4, 4096 blk)", 2 * arr, [&] { k_copy<true><<<4096, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
     timeit("copy (float4, 16384 blk)", 2 * arr, [&] { k_copy<false><<<16384, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
@@ -151,6 +319,22 @@ int main() {
     mimic(k_mimic<16>, 16, "mimic 4R+3W R=16");
     mimic(k_mimic<4>, 4, "mimic 4R+3W R=4");
     mimic(k_mimic<8, true>, 8, "mimic 4R+3W R=8 nt stores");
+    mimic(k_mimic2<8>, 8, "mimic2 4R+3W R=8, 2 rows/step");
+    mimic(k_mimic_perm<8>, 8, "mimic PERMUTED 4R+3W R=8");
+    mimic(k_mimic_perm<16>, 16, "mimic PERMUTED 4R+3W R=16");
+    mimic(k_mimic_perm<4>, 4, "mimic PERMUTED 4R+3W R=4");
+    mimic(k_mimic<8>, 8, "mimic 4R+3W R=8 (again)");
+    {
+        const long long ns = (long long)P * H / 8;
+        timeit("walk 1R+1W R=8", 2 * arr, [&] { k_walk11<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], H, ns); });
+        timeit("walkv contiguous R=8", 2 * arr, [&] { k_walkv<8, 0><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], H, ns, P); });
+        timeit("walkv row-interleaved R=8", 2 * arr, [&] { k_walkv<8, 1><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], H, ns, P); });
+        timeit("walkv plane-interleaved R=8", 2 * arr, [&] { k_walkv<8, 2><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], H, ns, P); });
+        const long long n1 = (long long)P * H;
+        timeit("walkv R=1", 2 * arr, [&] { k_walkv<1, 0><<<(unsigned)((n1 + 3) / 4), 256>>>(buf[0], buf[1], H, n1, P); });
+        const long long n32 = (long long)P * H / 32;
+        timeit("walkv contiguous R=32", 2 * arr, [&] { k_walkv<32, 0><<<(unsigned)((n32 + 3) / 4), 256>>>(buf[0], buf[1], H, n32, P); });
+    }
     mimic(k_mimic<4, true>, 4, "mimic 4R+3W R=4 nt stores");
     auto colm = [&](auto kern, int C, int tpb, const char* name) {
         const int colblocks = N / C;
@@ -161,6 +345,8 @@ int main() {
     colm(k_colmimic<16, 512>, 16, 512, "colmimic C=16 512 thr (E=32)");
     colm(k_colmimic<32, 1024>, 32, 1024, "colmimic C=32 1024 thr (E=32)");
     colm(k_colmimic<8, 256>, 8, 256, "colmimic C=8  256 thr (E=32)");
+    colm(k_colmimic_perm<8, 512, 8>, 8, 512, "colmimic PERMUTED C=8 512 thr");
+    colm(k_colmimic<8, 512>, 8, 512, "colmimic C=8  512 thr (again)");
     {
         const long long ns = (long long)P * H / 8;
         timeit("mimic interleaved u 3R+2W R=8", 7 * arr, [&] { k_mimic_il<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], ui, buf[3], uo, buf[6], H, ns); });

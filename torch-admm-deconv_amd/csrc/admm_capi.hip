@@ -424,7 +424,7 @@ GPlan make_plan(int n) {
     take_all(3);
     take_all(5);
     take_all(7);
-    for (int f = 11; m > 1; f += 2) take_all(f);  // any other prime: O(R) per output
+    for (int f = 11; f <= n && m > 1; f += 2) take_all(f);  // any other prime: O(R) per output
     return p;
 }
 
