@@ -271,6 +271,16 @@ template <int H> int pass_b_h(const cf* spec, cf* out, const float* fcT, const c
                               int mode, hipStream_t s) {
     constexpr int L = ColGeom<H, 1>::L;
     if constexpr (L <= 64) {
+        // column pairs with 16-byte accesses (k_pass_b2): measured faster up to H = 512 (C2: pass B
+        // -7.5 %, same bits); at H = 1024 the doubled register set costs occupancy (+30 %)
+        if (mode == 0 && N >= 16 && env_int("ADMM_PASSB_PAIR", H <= 512 ? 1 : 0)) {
+            using G = ColGeom<H, 8>;
+            const int colblocks = N / 16;
+            if (int e = set_lds(k_pass_b2<H, 8>, G::lds_bytes())) return e;
+            hipLaunchKernelGGL((k_pass_b2<H, 8>), dim3((unsigned)((long long)P * colblocks)), dim3(G::NT), G::lds_bytes(),
+                               s, spec, out, fcT, twH, N, colblocks);
+            return launch_check("k_pass_b2");
+        }
         int C = env_int("ADMM_PASSB_C", 8);
         if (C > N) C = N;
         if (C >= 16) return pass_b_hc<H, 16>(spec, out, fcT, mT, twH, N, P, mode, s);

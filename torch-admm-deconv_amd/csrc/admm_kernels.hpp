@@ -328,6 +328,88 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
     for (int j = 0; j < E; ++j) bstore_cf(ro, voff, j * sstep, v[j]);
 }
 
+// Pass B (MODE 0) with two adjacent columns per thread: 16-byte loads and stores, so the 8
+// lanes of a row segment move a whole 128-byte line (the 8-column kernel above moves 64-byte
+// halves).  The two column transforms of a thread run one after the other through the same
+// LDS exchange buffer (CP column pairs per block, LDS as for C = CP).
+#ifndef PASSB2_MINW
+#define PASSB2_MINW 4
+#endif
+__device__ __forceinline__ float4 bload_f4(rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore_f4(rsrc_t r, int voff, int soff, float4 v) {
+    typedef decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0)) V4;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(V4, v), r, voff, soff, 0);
+}
+
+template <int H, int CP>
+__global__ void __launch_bounds__(CP * (H / RowCfg<H>::E), PASSB2_MINW)
+    k_pass_b2(const cf* spec_in, cf* spec_out, const float* __restrict__ fcT, const cf* __restrict__ twH_g, int N,
+              int colblocks) {
+    using G = ColGeom<H, CP>;
+    constexpr int E = G::E, L = G::L;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* data = tw + H;
+    load_tw(tw, twH_g, H);
+    const int tid = threadIdx.x;
+    const int cp = tid % CP, t = tid / CP;
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int p = lb / colblocks, cb = lb % colblocks;
+    const int col = cb * 2 * CP + 2 * cp;  // this thread's columns: col, col + 1
+    const rsrc_t rs = make_rsrc(spec_in + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+    const rsrc_t ro = make_rsrc(spec_out + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+    const int voff = (t * N + col) * (int)sizeof(cf);
+    const int sstep = L * N * (int)sizeof(cf);
+    cf v0[E], v1[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const float4 q = bload_f4(rs, voff, j * sstep);
+        v0[j] = mkc(q.x, q.y);
+        v1[j] = mkc(q.z, q.w);
+    }
+    // Wiener factors of the two columns (L2-resident table); the second set is loaded only
+    // after the first column is done, to keep the register footprint at one set
+    const rsrc_t rm = make_rsrc(fcT, (unsigned)((size_t)(N + 1) * H * sizeof(float)));
+    const int mo = (col * H + t) * (int)sizeof(float);
+    float m0[E], m1[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) m0[j] = bload_f(rm, mo, j * L * (int)sizeof(float));
+    __syncthreads();
+    ColBuf<CP> buf{data + cp};
+    fft<H, L, -1, 1, 1>(v0, buf, tw, t);
+    if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H-ky]
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < E; ++j) buf.at(t + L * j) = v0[j];
+        __syncthreads();
+        if (col == 0) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int ky = t + L * j;
+                const cf q = cconj(buf.at((H - ky) & (H - 1)));
+                const float f0 = m0[j], fn = fcT[(size_t)N * H + ky];
+                const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
+                v0[j] = mkc(fmaf(a, v0[j].x, b * q.x), fmaf(a, v0[j].y, b * q.y));
+            }
+        }
+    }
+    if (col != 0) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) v0[j] = cscale(v0[j], m0[j]);
+    }
+    fft<H, L, +1, 1, 1>(v0, buf, tw, t);
+#pragma unroll
+    for (int j = 0; j < E; ++j) m1[j] = bload_f(rm, mo + H * (int)sizeof(float), j * L * (int)sizeof(float));
+    fft<H, L, -1, 1, 1>(v1, buf, tw, t);
+#pragma unroll
+    for (int j = 0; j < E; ++j) v1[j] = cscale(v1[j], m1[j]);
+    fft<H, L, +1, 1, 1>(v1, buf, tw, t);
+#pragma unroll
+    for (int j = 0; j < E; ++j) bstore_f4(ro, voff, j * sstep, make_float4(v0[j].x, v0[j].y, v1[j].x, v1[j].y));
+}
+
 // ---------------------------------------------------------------------------
 // pass A: the fused row pass of one ADMM iteration, one sub-group per strip of R rows
 //
