@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ADMM_TV_ABI_VERSION 2
+#define ADMM_TV_ABI_VERSION 3
 
 enum {
     ADMM_TV_OK = 0,
@@ -47,13 +47,21 @@ enum {
  * (deconv.py:35-42): xin (B,C,H,W), kern (1,1,kh,kw) or empty (kh = kw = 0),
  * iso (False = soft/anisotropic shrink, True = block shrink with the per-pixel
  * norm over batch AND channel, deconv.py:19-24), maxit (>= 0).
- * Supported on the device path: H in {16..4096}, W in {16..2048}, powers of two. */
+ * Sizes: see admm_tv_supported.
+ *
+ * groups (0 or 1: one solve): G > 1 solves G modules that share the input xin and the
+ * PSF but have their own lambda[g], rho[g] (device arrays of G floats) in one pass
+ * sequence -- the two ADMMDeconv modules of DivergentAttention's first level
+ * (blocks.py:187-196).  out / gout / history then hold G*B*C planes (module-major),
+ * glam / grho G values, gxin the sum over modules.  Each module's iso norm runs over its
+ * own (B,C).  Fused power-of-two sizes only, no PSF gradient. */
 typedef struct admm_tv_desc {
     int64_t B, C, H, W;
     int32_t kh, kw;
     int32_t iso;
     int32_t maxit;
     int32_t flags;   /* ADMM_TV_FLAG_*; 0 for plain use */
+    int32_t groups;  /* modules solved together (0 or 1: one) */
 } admm_tv_desc;
 
 /* flags: the training forward also keeps the spectra of every r_k so that

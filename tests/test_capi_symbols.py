@@ -49,7 +49,7 @@ def test_library_is_gfx950_code():
 def test_host_entry_points():
     from admmtor import _native
     lib = _native.load()
-    assert lib.admm_tv_abi_version() == 2
+    assert lib.admm_tv_abi_version() == 3
     fast, generic = 1, 2
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
     assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 4096), (8, 64), (1, 1), (481, 321))] == [generic] * 5
@@ -82,3 +82,20 @@ def test_psf_larger_than_image_is_rejected():
     d = _native.desc(1, 1, 16, 16, 21, False, 5)
     n = ctypes.c_size_t(0)
     assert _native.load().admm_tv_workspace_size(ctypes.byref(d), ctypes.byref(n)) == -6
+
+
+def test_groups_descriptor():
+    """desc.groups = G: G modules sharing xin -> G x the per-plane state, G Wiener factors."""
+    from admmtor import _native
+    one = _native.workspace_size(_native.desc(16, 3, 512, 512, 0, True, 100))
+    two = _native.workspace_size(_native.desc(16, 3, 512, 512, 0, True, 100, 0, 2))
+    assert 1.8 * one < two < 2.1 * one
+    h1 = _native.history_size(_native.desc(16, 3, 512, 512, 0, True, 10))
+    h2 = _native.history_size(_native.desc(16, 3, 512, 512, 0, True, 10, 0, 2))
+    assert abs(h2 - 2 * h1) < (1 << 16)
+    n = ctypes.c_size_t(0)
+    lib = _native.load()
+    # generic sizes and PSF gradients are not grouped
+    assert lib.admm_tv_workspace_size(ctypes.byref(_native.desc(1, 1, 15, 17, 0, False, 5, 0, 2)), ctypes.byref(n)) == -2
+    assert lib.admm_tv_workspace_size(ctypes.byref(_native.desc(1, 1, 64, 64, 3, False, 5, 1, 2)), ctypes.byref(n)) == -2
+    assert lib.admm_tv_workspace_size(ctypes.byref(_native.desc(1, 1, 64, 64, 0, False, 5, 0, -1)), ctypes.byref(n)) == -1

@@ -53,6 +53,7 @@ def _cpu_cnn(g, leaves):
 def test_model_split_at_solver_vs_reference(cuda_dev):
     g = load_golden("g8_model_admm")
     m = _model(g, cuda_dev)
+    m.blocks[0].group_admms = False  # per-module calls, so the forward hooks below see each solve
     captured = []
     hooks = [a.register_forward_hook(lambda mod, i, o: captured.append(o)) for a in m.blocks[0].admms]
     x = torch.from_numpy(g["x"]).float().to(cuda_dev).requires_grad_(True)
@@ -130,3 +131,26 @@ def test_model_bf16_autocast_train_step(cuda_dev):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         ref = m(x)
     assert rel(ref.float().detach().cpu(), out.float().detach().cpu()) < 0.5
+
+
+def test_grouped_admm_modules_match_separate(cuda_dev):
+    """DivergentAttention solves its two ADMM modules in one grouped native call (desc.groups = 2);
+    outputs and every gradient match the per-module calls."""
+    g = load_golden("g8_model_admm")
+    res = []
+    for grouped in (False, True):
+        m = _model(g, cuda_dev)
+        m.blocks[0].group_admms = grouped
+        x = torch.from_numpy(g["x"]).float().to(cuda_dev).requires_grad_(True)
+        out = m(x)
+        (out * torch.from_numpy(g["cot"]).float().to(cuda_dev)).sum().backward()
+        res.append((out.detach().cpu(), x.grad.cpu(),
+                    {k: p.grad.cpu() for k, p in m.named_parameters() if p.grad is not None}))
+    (o0, gx0, p0), (o1, gx1, p1) = res
+    print("grouped vs separate: out", rel(o1, o0), "x.grad", rel(gx1, gx0),
+          "lambda/rho", [(k, rel(p1[k], p0[k])) for k in p0 if ".admms." in k])
+    assert sorted(p0) == sorted(p1)
+    assert rel(o1, o0) <= 1e-6 and rel(gx1, gx0) <= 1e-5
+    for k in p0:
+        if ".admms." in k:
+            assert rel(p1[k], p0[k]) <= 1e-5, k

@@ -39,15 +39,16 @@ class AdmmTvFunction(torch.autograd.Function):
     def forward(ctx, x32, lam, rho, k32, iso: bool, maxit: int, hook=None, psf_grad: bool = False):
         lib = _native.load()
         B, C, H, W = x32.shape
+        G = lam.numel()  # > 1: modules sharing x32 (fft_admm_tv_grouped); output (G B, C, H, W)
         k = int(k32.shape[-1]) if k32.numel() > 0 else 0
         flags = _native.ADMM_TV_FLAG_PSF_GRAD if (psf_grad and k > 0) else 0
-        d = _native.desc(B, C, H, W, k, iso, maxit, flags)
+        d = _native.desc(B, C, H, W, k, iso, maxit, flags, G)
         x32 = x32.contiguous()
         k32c = k32.contiguous()
         lam_c, rho_c = lam.contiguous(), rho.contiguous()
         ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
         hist = torch.empty(max(_native.history_size(d), 1), dtype=torch.uint8, device=x32.device)
-        out = torch.empty_like(x32)
+        out = torch.empty((G * B, C, H, W), dtype=torch.float32, device=x32.device)
         stream = torch.cuda.current_stream(x32.device).cuda_stream
         hook = hook if iso else None
         with (hook if hook is not None else contextlib.nullcontext()):
@@ -59,14 +60,14 @@ class AdmmTvFunction(torch.autograd.Function):
         ctx.hook = hook
         ctx.save_for_backward(k32c, lam_c, rho_c, x32 if flags else None)
         ctx.hist = hist
-        ctx.desc = (B, C, H, W, k, iso, maxit, flags)
+        ctx.desc = (B, C, H, W, k, iso, maxit, flags, G)
         return out
 
     @staticmethod
     def backward(ctx, gout):
         k32, lam, rho, x32 = ctx.saved_tensors
-        B, C, H, W, k, iso, maxit, flags = ctx.desc
-        d = _native.desc(B, C, H, W, k, iso, maxit, flags)
+        B, C, H, W, k, iso, maxit, flags, G = ctx.desc
+        d = _native.desc(B, C, H, W, k, iso, maxit, flags, G)
         need_k = ctx.needs_input_grad[3] and k > 0
         if need_k and not flags:
             raise RuntimeError("admmtor: PSF gradient requested but the forward did not keep the spectra")
@@ -76,8 +77,8 @@ class AdmmTvFunction(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0]
         need_s = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
         gx = torch.empty((B, C, H, W), dtype=torch.float32, device=dev) if need_x else None
-        gl = torch.empty(1, dtype=torch.float32, device=dev) if need_s else None
-        gr = torch.empty(1, dtype=torch.float32, device=dev) if need_s else None
+        gl = torch.empty(G, dtype=torch.float32, device=dev) if need_s else None
+        gr = torch.empty(G, dtype=torch.float32, device=dev) if need_s else None
         gk = torch.empty((1, 1, k, k), dtype=torch.float32, device=dev) if need_k else None
         ws = torch.empty(_native.backward_workspace_size(d), dtype=torch.uint8, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
@@ -108,3 +109,15 @@ def fft_admm_tv_autograd(xin, lmbd, rho, kern, iso, maxit, hook=None):
     psf_grad = isinstance(kern, torch.Tensor) and kern.requires_grad and kern.numel() > 0
     out = AdmmTvFunction.apply(x32, lam_t, rho_t, k32, bool(iso), int(maxit), hook, psf_grad)
     return out
+
+
+def fft_admm_tv_grouped_autograd(xin, lmbds, rhos, kern, iso, maxit):
+    """G modules sharing xin (eops.deconv.fft_admm_tv_grouped) with the native backward: lambda and
+    rho are stacked into (G,) tensors (differentiably, so each module's parameters get theirs)."""
+    dev = xin.device
+    x32 = xin.to(torch.float32)
+    k32 = kern.detach().to(device=dev, dtype=torch.float32) if kern.numel() > 0 else \
+        torch.empty(0, dtype=torch.float32, device=dev)
+    lam_t = torch.cat([_scalar_input(v, dev)[0] for v in lmbds])
+    rho_t = torch.cat([_scalar_input(v, dev)[0] for v in rhos])
+    return AdmmTvFunction.apply(x32, lam_t, rho_t, k32, bool(iso), int(maxit), None, False)

@@ -50,11 +50,12 @@ class AdmmTvDesc(ctypes.Structure):
         ("iso", ctypes.c_int32),
         ("maxit", ctypes.c_int32),
         ("flags", ctypes.c_int32),
+        ("groups", ctypes.c_int32),
     ]
 
 
 ADMM_TV_FLAG_PSF_GRAD = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
@@ -130,8 +131,9 @@ def check(code: int) -> None:
         raise NativeError(code, msg)
 
 
-def desc(B, C, H, W, k, iso, maxit, flags=0) -> AdmmTvDesc:
-    return AdmmTvDesc(int(B), int(C), int(H), int(W), int(k), int(k), int(bool(iso)), int(maxit), int(flags))
+def desc(B, C, H, W, k, iso, maxit, flags=0, groups=1) -> AdmmTvDesc:
+    return AdmmTvDesc(int(B), int(C), int(H), int(W), int(k), int(k), int(bool(iso)), int(maxit), int(flags),
+                      int(groups))
 
 
 def workspace_size(d: AdmmTvDesc) -> int:

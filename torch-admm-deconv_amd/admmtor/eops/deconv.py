@@ -114,12 +114,13 @@ def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.T
     `hook`: an _native.AllReduceHook for iso over a batch sharded across ranks."""
     lib = _native.load()
     B, C, H, W = x32.shape
+    G = lam.numel()  # modules solved together (fft_admm_tv_grouped); 1 for fft_admm_tv
     k = int(k32.shape[-1]) if k32.numel() > 0 else 0
-    d = _native.desc(B, C, H, W, k, iso, maxit)
+    d = _native.desc(B, C, H, W, k, iso, maxit, 0, G)
     if not _native.supported(H, W):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} outside [1, 4096]")
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
-    out = torch.empty_like(x32)
+    out = torch.empty((G * B, C, H, W), dtype=torch.float32, device=x32.device)
     stream = torch.cuda.current_stream(x32.device).cuda_stream
     with (hook if (hook is not None and iso) else contextlib.nullcontext()):
         _native.register_buffers(ws)
@@ -169,3 +170,43 @@ def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> 
         from .._backward import fft_admm_tv_autograd
         return fft_admm_tv_autograd(xin, lmbd, rho, kern, bool(iso), maxit, hook=hook)
     return _solve(x32, k32, lam, rh, bool(iso), maxit, hook=hook)
+
+
+def fft_admm_tv_grouped(xin: torch.Tensor, lmbds, rhos, kern: torch.Tensor, iso: bool = False,
+                        maxit: int = 100) -> list:
+    """G ADMM-TV solves of the SAME input with per-module lambda / rho, in one pass sequence.
+
+    ``[fft_admm_tv(xin, l, r, kern, iso, maxit) for l, r in zip(lmbds, rhos)]`` as one native
+    call (desc.groups = G): every launch covers all modules' planes, each module keeps its own
+    Wiener factor (its rho) and, for iso, its own per-pixel norm over its (B, C).  This is how
+    DivergentAttention's ADMM modules that share x run (blocks.py:187-196).
+    Autograd reaches xin (summed over modules) and every lambda / rho.  Needs power-of-two
+    H, W on the fused kernels and a PSF that does not require grad; returns G tensors.
+    """
+    if not isinstance(kern, torch.Tensor):
+        kern = torch.as_tensor(kern)
+    _check_inputs(xin, kern)
+    if not xin.is_cuda:
+        raise RuntimeError("admmtor (MI355X build): fft_admm_tv runs on ROCm device tensors only; "
+                           "move xin (and kern) to the GPU. There is no CPU path.")
+    G = len(lmbds)
+    if G != len(rhos) or G < 1:
+        raise ValueError("lmbds and rhos must have the same, non-zero length")
+    B, C, H, W = xin.shape
+    if _native.load().admm_tv_supported(H, W) != 1 or (kern.requires_grad and kern.numel() > 0):
+        raise NotImplementedError("grouped solve: power-of-two H, W (fused kernels) and a fixed PSF only")
+    maxit = max(0, int(maxit))
+    dev = xin.device
+    needs_grad = torch.is_grad_enabled() and (
+        xin.requires_grad or any(isinstance(v, torch.Tensor) and v.requires_grad for v in (*lmbds, *rhos)))
+    if needs_grad:
+        from .._backward import fft_admm_tv_grouped_autograd
+        out = fft_admm_tv_grouped_autograd(xin, lmbds, rhos, kern, bool(iso), maxit)
+    else:
+        x32 = xin.detach().to(torch.float32).contiguous()
+        k32 = kern.detach().to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \
+            torch.empty(0, dtype=torch.float32, device=dev)
+        lam = torch.cat([_as_device_scalar(v, dev) for v in lmbds])
+        rh = torch.cat([_as_device_scalar(v, dev) for v in rhos])
+        out = _solve(x32, k32, lam, rh, bool(iso), maxit)
+    return list(out.split(B, dim=0))

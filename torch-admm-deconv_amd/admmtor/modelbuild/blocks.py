@@ -17,6 +17,7 @@ from torch.utils.checkpoint import checkpoint
 
 from admmtor.elayers.admmdeconv import ADMMDeconv
 from admmtor.elayers.attentions import CBAM
+from admmtor.eops.deconv import fft_admm_tv_grouped
 
 
 @torch.no_grad()
@@ -122,19 +123,33 @@ class DivergentAttention(nn.Module):
         # recompute each conv+attention branch in the backward instead of keeping its
         # activations (off by default; see set_branch_checkpointing)
         self.checkpoint_branches = False
+        # solve ADMM modules that share x together (see _admm_outputs); plain attribute, not state
+        self.group_admms = True
 
-    def _features(self, x, idx):
-        """Conv branch `idx` applied to x (or to the idx-th ADMM restoration of x)."""
-        if self.admms is None:
-            return self.convs[idx](x)
-        return self.convs[idx](self.admms[idx](x))
+    def _admm_outputs(self, x):
+        """Every ADMM module applied to x.  Modules that differ only in lambda / rho (no PSF, the
+        same iterations and shrink -- train.py's DECONV1/DECONV2) are solved together in one
+        native pass sequence (fft_admm_tv_grouped, desc.groups); otherwise one call each."""
+        mods = list(self.admms)
+        groupable = (self.group_admms and len(mods) > 1 and x.is_cuda and x.dim() == 4
+                     and all(m.w.numel() == 0 and m.max_iters == mods[0].max_iters and m.iso == mods[0].iso
+                             for m in mods))
+        if groupable:
+            from admmtor import _native
+            groupable = _native.load().admm_tv_supported(x.shape[-2], x.shape[-1]) == 1
+        if not groupable:
+            return [m(x) for m in mods]
+        sols = fft_admm_tv_grouped(x, [m.lmbda for m in mods], [m.rho for m in mods], mods[0].w,
+                                   mods[0].iso, mods[0].max_iters)
+        return [m.activation(sol + m.b) for m, sol in zip(mods, sols)]  # ADMMDeconv.forward's tail
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         n_convs = len(self.convs) if self.admms is None else min(len(self.convs), len(self.admms))
         first, second = _branch_plan(n_convs, len(self.attentions))
+        restored = self._admm_outputs(x) if self.admms is not None else None
 
         def branch(a, o, inp):
-            f = self._features(inp, o)
+            f = self.convs[o](inp if restored is None else restored[o])
             return self.attentions[a](f) + f
 
         def gated(pairs):

@@ -42,6 +42,7 @@ struct BwdArgs {
     const cf* twW;
     int H, R;
     long long nstrips;
+    long long ppm;        // planes per module (PassAArgs): lam/rho[m], np/qp + m 2HW
 };
 
 // S'(a) contracted with z^: aniso mask, iso block Jacobian (f z^ + 2 a f'(N) Q)
@@ -79,8 +80,10 @@ __global__ void __launch_bounds__(256) k_bwd_pass_a(BwdArgs a) {
     const long long p = strip / spp;
     const int i0 = (int)(strip % spp) * R;
     RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
-    const float rho = a.rho[0];
-    const float tau = a.lam[0] / rho;
+    const int mod = (int)(p / a.ppm);
+    const float rho = a.rho[mod];
+    const float tau = a.lam[mod] / rho;
+    const size_t moff = (size_t)mod * 2 * H * W;
 
     const cf* sp = a.sin + (size_t)p * H * N;
     cf* so = a.sout + (size_t)p * H * N;
@@ -95,10 +98,10 @@ __global__ void __launch_bounds__(256) k_bwd_pass_a(BwdArgs a) {
     const cf* aky = img(a.aky);
     const cf* apx = FIRSTK ? nullptr : img(a.apx);
     const cf* apy = FIRSTK ? nullptr : img(a.apy);
-    const cf* npx = reinterpret_cast<const cf*>(a.np);
-    const cf* npy = reinterpret_cast<const cf*>(a.np + (size_t)H * W);
-    const cf* qpx = reinterpret_cast<const cf*>(a.qp);
-    const cf* qpy = reinterpret_cast<const cf*>(a.qp + (size_t)H * W);
+    const cf* npx = reinterpret_cast<const cf*>(a.np + moff);
+    const cf* npy = reinterpret_cast<const cf*>(a.np + moff + (size_t)H * W);
+    const cf* qpx = reinterpret_cast<const cf*>(a.qp + moff);
+    const cf* qpy = reinterpret_cast<const cf*>(a.qp + moff + (size_t)H * W);
 
     float rho_acc = 0.f, tau_acc = 0.f;
     cf rprev[E], rcur[E], abxp[E], abyp[E];
@@ -255,6 +258,7 @@ struct BwdIsoArgs {
     const cf* twW;
     int P, H, ppg;
     long long nitems;
+    long long ppm;       // planes per module
 };
 
 template <int N, bool LASTK>
@@ -273,7 +277,7 @@ __global__ void __launch_bounds__(256) k_bwd_iso_q(BwdIsoArgs a) {
     const int grp = (int)(item / H);
     const int gm = (g - 1 + H) & (H - 1);
     RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
-    const float rho = a.rho[0];
+    const float rho = a.rho[(long long)grp * a.ppg / a.ppm];
     cf qx[E], qy[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) qx[j] = qy[j] = mkc(0.f, 0.f);
@@ -341,18 +345,25 @@ __global__ void k_iso_tau_partial(const float* __restrict__ q, const float* __re
     if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
-// final scalars: tau^ = sum of partials, rho^ = sum + tau^ * (-lam / rho^2), lam^ = tau^ / rho
-// (single block, fixed order -> deterministic)
-__global__ void k_bwd_scalars(const float* __restrict__ part, long long nstrip_parts, const float* __restrict__ tpart,
-                              int ntp, const float* __restrict__ lam, const float* __restrict__ rho,
-                              float* __restrict__ glam, float* __restrict__ grho) {
+// final scalars of one module: tau^ = sum of its partials, rho^ = sum + tau^ * (-lam / rho^2),
+// lam^ = tau^ / rho.  part: [K][nstrips][2], the module's strips at [soff, soff + spm) of every
+// iteration; tpart (iso, or null): [K][G][ntp].  Single block, fixed order -> deterministic.
+__global__ void k_bwd_scalars(const float* __restrict__ part, int K, long long nstrips, long long spm, long long soff,
+                              const float* __restrict__ tpart, int ntp, int G, int g, const float* __restrict__ lam,
+                              const float* __restrict__ rho, float* __restrict__ glam, float* __restrict__ grho) {
     __shared__ double r1[256], r2[256];
     double sr = 0.0, st = 0.0;
-    for (long long i = threadIdx.x; i < nstrip_parts; i += blockDim.x) {
-        sr += part[2 * i + 0];
-        st += part[2 * i + 1];
+    for (int it = 0; it < K; ++it) {
+        const float* pp = part + ((size_t)it * nstrips + soff) * 2;
+        for (long long i = threadIdx.x; i < spm; i += blockDim.x) {
+            sr += pp[2 * i + 0];
+            st += pp[2 * i + 1];
+        }
+        if (tpart) {
+            const float* tp = tpart + ((size_t)it * G + g) * ntp;
+            for (int i = threadIdx.x; i < ntp; i += blockDim.x) st += tp[i];
+        }
     }
-    for (int i = threadIdx.x; i < ntp; i += blockDim.x) st += tpart[i];
     r1[threadIdx.x] = sr;
     r2[threadIdx.x] = st;
     __syncthreads();
@@ -369,6 +380,21 @@ __global__ void k_bwd_scalars(const float* __restrict__ part, long long nstrip_p
         glam[0] = (float)(tb / r);
         grho[0] = (float)(r1[0] - tb * l / (r * r));
     }
+}
+
+// sum of the modules' b^ images: out[i] = sum_g in[g n + i] (fixed order)
+__global__ void k_sum_modules(const float4* __restrict__ in, float4* __restrict__ out, int G, long long n4) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    float4 s = in[i];
+    for (int g = 1; g < G; ++g) {
+        const float4 q = in[(size_t)g * n4 + i];
+        s.x += q.x;
+        s.y += q.y;
+        s.z += q.z;
+        s.w += q.w;
+    }
+    out[i] = s;
 }
 
 // accumulate per-iteration scalar partials into a running [2] (rho^, tau^) pair in fp64-free fixed order

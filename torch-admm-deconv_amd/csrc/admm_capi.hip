@@ -90,6 +90,9 @@ bool generic_hw(int64_t H, int64_t W) {
     return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax;
 }
 
+// modules solved together (admm_tv_desc.groups)
+int ngroups_of(const admm_tv_desc& d) { return d.groups > 1 ? d.groups : 1; }
+
 constexpr size_t kAlign = 256;
 size_t up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
@@ -102,8 +105,10 @@ struct Layout {
 
 Layout make_layout(const admm_tv_desc& d) {
     Layout L{};
-    const size_t P = (size_t)d.B * d.C, H = d.H, W = d.W, N = W / 2;
+    const size_t G = ngroups_of(d);
+    const size_t P = (size_t)d.B * d.C * G, H = d.H, W = d.W, N = W / 2;  // all modules' planes
     const size_t img = P * H * W * sizeof(float);
+    const size_t img_m = (size_t)d.B * d.C * H * W * sizeof(float);         // one module's planes
     const int k = d.kh;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -116,8 +121,8 @@ Layout make_layout(const admm_tv_desc& d) {
     L.spec[1] = take(img);
     L.rimg = L.gen ? take(img) : 0;
     for (int i = 0; i < 4; ++i) L.u[i] = take(img);
-    L.b = k > 0 ? take(img) : 0;
-    L.fcT = take((N + 1) * H * sizeof(float));
+    L.b = k > 0 ? take(img_m) : 0;  // b = H_t(xin) is shared by the modules
+    L.fcT = take(G * (N + 1) * H * sizeof(float));  // one Wiener factor per module (its rho)
     L.mT = take((N + 1) * H * sizeof(cf));
     L.twW = take(W * sizeof(cf));
     L.twH = take(H * sizeof(cf));
@@ -128,10 +133,15 @@ Layout make_layout(const admm_tv_desc& d) {
         // plane groups for the iso norm pass: enough (group,row) items to fill the chip
         int ppg = 8;
         if ((size_t)P <= 8) ppg = (int)P;
+        if (G > 1) {  // a plane group must not straddle two modules: a divisor of B*C
+            const int pm = (int)(d.B * d.C);
+            ppg = std::min(8, pm);
+            while (pm % ppg) --ppg;
+        }
         L.ppg = ppg;
         L.ngroups = (int)((P + ppg - 1) / ppg);
         L.part = take((size_t)L.ngroups * 2 * H * W * sizeof(float));
-        L.nsq = take(2 * H * W * sizeof(float));
+        L.nsq = take(G * 2 * H * W * sizeof(float));  // per module
     }
     L.total = o;
     return L;
@@ -250,25 +260,25 @@ template <class F> int with_row(int N, F&& f) {
 
 // ------------------------------------------------------------------ column-side ops (templated on H, C)
 template <int H, int C> int pass_b_hc(const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N,
-                                      int P, int mode, hipStream_t s) {
+                                      int P, int mode, int ppm, hipStream_t s) {
     using G = ColGeom<H, C>;
     const int colblocks = N / C;
     const dim3 grid((unsigned)((long long)P * colblocks));
     if (mode == 0) {
         if (int e = set_lds(k_pass_b<H, C, 0>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks);
+        hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm);
     } else if (mode == 1) {
         if (int e = set_lds(k_pass_b<H, C, 1>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks);
+        hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm);
     } else {
         if (int e = set_lds(k_pass_b<H, C, 2>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks);
+        hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm);
     }
     return launch_check("k_pass_b");
 }
 
 template <int H> int pass_b_h(const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N, int P,
-                              int mode, hipStream_t s) {
+                              int mode, int ppm, hipStream_t s) {
     constexpr int L = ColGeom<H, 1>::L;
     if constexpr (L <= 64) {
         // column pairs with 16-byte accesses (k_pass_b2): measured faster up to H = 512 (C2: pass B
@@ -278,39 +288,42 @@ template <int H> int pass_b_h(const cf* spec, cf* out, const float* fcT, const c
             const int colblocks = N / 16;
             if (int e = set_lds(k_pass_b2<H, 8>, G::lds_bytes())) return e;
             hipLaunchKernelGGL((k_pass_b2<H, 8>), dim3((unsigned)((long long)P * colblocks)), dim3(G::NT), G::lds_bytes(),
-                               s, spec, out, fcT, twH, N, colblocks);
+                               s, spec, out, fcT, twH, N, colblocks, ppm);
             return launch_check("k_pass_b2");
         }
         int C = env_int("ADMM_PASSB_C", 8);
         if (C > N) C = N;
-        if (C >= 16) return pass_b_hc<H, 16>(spec, out, fcT, mT, twH, N, P, mode, s);
-        return pass_b_hc<H, 8>(spec, out, fcT, mT, twH, N, P, mode, s);
+        if (C >= 16) return pass_b_hc<H, 16>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        return pass_b_hc<H, 8>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
     } else if constexpr (L == 128) {
-        return pass_b_hc<H, 8>(spec, out, fcT, mT, twH, N, P, mode, s);
+        return pass_b_hc<H, 8>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
     } else {
-        return pass_b_hc<H, 4>(spec, out, fcT, mT, twH, N, P, mode, s);
+        return pass_b_hc<H, 4>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
     }
 }
 
 // column pass; out == spec (in place) or a separate buffer
+// ppm: planes per module (module m = plane / ppm uses Wiener factor m); ppm = P for one module
 int pass_b_oop(int H, const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode,
-               hipStream_t s) {
+               hipStream_t s, int ppm = 0) {
+    if (ppm <= 0) ppm = P;
     switch (H) {
-        case 16: return pass_b_h<16>(spec, out, fcT, mT, twH, N, P, mode, s);
-        case 32: return pass_b_h<32>(spec, out, fcT, mT, twH, N, P, mode, s);
-        case 64: return pass_b_h<64>(spec, out, fcT, mT, twH, N, P, mode, s);
-        case 128: return pass_b_h<128>(spec, out, fcT, mT, twH, N, P, mode, s);
-        case 256: return pass_b_h<256>(spec, out, fcT, mT, twH, N, P, mode, s);
-        case 512: return pass_b_h<512>(spec, out, fcT, mT, twH, N, P, mode, s);
-        case 1024: return pass_b_h<1024>(spec, out, fcT, mT, twH, N, P, mode, s);
-        case 2048: return pass_b_h<2048>(spec, out, fcT, mT, twH, N, P, mode, s);
-        case 4096: return pass_b_h<4096>(spec, out, fcT, mT, twH, N, P, mode, s);
+        case 16: return pass_b_h<16>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        case 32: return pass_b_h<32>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        case 64: return pass_b_h<64>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        case 128: return pass_b_h<128>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        case 256: return pass_b_h<256>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        case 512: return pass_b_h<512>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        case 1024: return pass_b_h<1024>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        case 2048: return pass_b_h<2048>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
+        case 4096: return pass_b_h<4096>(spec, out, fcT, mT, twH, N, P, mode, ppm, s);
         default: return fail(ADMM_TV_EUNSUPPORTED, "unsupported H");
     }
 }
 
-int pass_b(int H, cf* spec, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode, hipStream_t s) {
-    return pass_b_oop(H, spec, spec, fcT, mT, twH, N, P, mode, s);
+int pass_b(int H, cf* spec, const float* fcT, const cf* mT, const cf* twH, int N, int P, int mode, hipStream_t s,
+           int ppm = 0) {
+    return pass_b_oop(H, spec, spec, fcT, mT, twH, N, P, mode, s, ppm);
 }
 
 // cross-spectrum partials sum_{p in group} conj(colFFT U_p) colFFT V_p  -> part[g][N+1][H]
@@ -351,12 +364,14 @@ int xspec(int H, const cf* U, const cf* V, cf* part, const cf* twH, int N, int P
 
 int validate(const admm_tv_desc* d) {
     if (!d) return fail(ADMM_TV_EINVAL, "null descriptor");
-    if (d->B <= 0 || d->C <= 0 || d->H <= 0 || d->W <= 0 || d->maxit < 0 || d->kh < 0 || d->kw < 0)
+    if (d->B <= 0 || d->C <= 0 || d->H <= 0 || d->W <= 0 || d->maxit < 0 || d->kh < 0 || d->kw < 0 || d->groups < 0)
         return fail(ADMM_TV_EINVAL, "invalid sizes or maxit");
     if (d->kh != d->kw) return fail(ADMM_TV_ENONSQUARE, "non-square PSF (the reference's H_t swaps H/W pads)");
     if (!supported_hw(d->H, d->W) && !generic_hw(d->H, d->W))
         return fail(ADMM_TV_EUNSUPPORTED, "H and W must be in [1, 4096]");
     if (d->kh > d->H || d->kw > d->W) return fail(ADMM_TV_EKERNEL, "PSF larger than the image");
+    if (d->groups > 1 && (!supported_hw(d->H, d->W) || (d->flags & ADMM_TV_FLAG_PSF_GRAD)))
+        return fail(ADMM_TV_EUNSUPPORTED, "groups > 1 needs power-of-two H, W and no PSF gradient");
     return 0;
 }
 
@@ -381,10 +396,12 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
     }
     const int n = (N + 1) * H;
     if (rho) {
-        hipLaunchKernelGGL(k_spectra, dim3((n + nt - 1) / nt), dim3(nt), 0, s, at<double2>(ws, Lo.G),
-                           at<double2>(ws, Lo.twHd), rho, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), k, H, N, W,
-                           Lo.sigma ? at<double2>(ws, Lo.sigma) : nullptr, spectra_scale(H, W));
-        if (int e = launch_check("k_spectra")) return e;
+        for (int g = 0; g < ngroups_of(d); ++g) {  // one Wiener factor per module
+            hipLaunchKernelGGL(k_spectra, dim3((n + nt - 1) / nt), dim3(nt), 0, s, at<double2>(ws, Lo.G),
+                               at<double2>(ws, Lo.twHd), rho + g, at<float>(ws, Lo.fcT) + (size_t)g * n, at<cf>(ws, Lo.mT),
+                               k, H, N, W, Lo.sigma ? at<double2>(ws, Lo.sigma) : nullptr, spectra_scale(H, W));
+            if (int e = launch_check("k_spectra")) return e;
+        }
     }
     return 0;
 }
@@ -540,9 +557,10 @@ struct Hist {
 };
 Hist make_hist(const admm_tv_desc& d) {
     Hist h{};
-    const size_t img = (size_t)d.B * d.C * d.H * d.W * sizeof(float);
+    const size_t G = ngroups_of(d);
+    const size_t img = G * d.B * d.C * d.H * d.W * sizeof(float);
     h.a_slot = up(img);
-    h.n_slot = d.iso ? up(2 * (size_t)d.H * d.W * sizeof(float)) : 0;
+    h.n_slot = d.iso ? up(G * 2 * (size_t)d.H * d.W * sizeof(float)) : 0;
     h.n_off = (size_t)d.maxit * 2 * h.a_slot;
     h.t_off = h.n_off + (size_t)d.maxit * h.n_slot;
     h.keep_t = d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD);
@@ -650,7 +668,8 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     const Layout Lo = make_layout(d);
     if (!ws || ws_bytes < Lo.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
         return fail(ADMM_TV_EWORKSPACE, "workspace too small or not 256-byte aligned");
-    const long long P = d.B * d.C;
+    const int G = ngroups_of(d);
+    const long long Pm = d.B * d.C, P = G * Pm;  // planes of one module, of all modules
     const int H = (int)d.H, W = (int)d.W, N = W / 2;
     const size_t img_bytes = (size_t)P * H * W * sizeof(float);
     if (d.maxit == 0) {
@@ -687,10 +706,10 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         if (int e = psf_transpose_into(d, Lo, ws, xin, bb, spec[0], 1, s)) return e;
         bimg = bb;
     }
-    {
+    for (int g = 0; g < G; ++g) {  // r_1 = b for every module
         ProfScope ps(3, s);
-        cf* t0 = keep_t ? ht(1) : spec[0];
-        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, t0, twW, rows, s); });
+        cf* t0 = (keep_t ? ht(1) : spec[0]) + (size_t)g * Pm * H * N;
+        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, t0, twW, Pm * H, s); });
         if (e) return e;
     }
     const int R = strip_rows(H, N, rows);
@@ -701,7 +720,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
             ProfScope ps(1, s);
             // PSF-gradient training keeps r_k's spectrum: the column pass then runs out of place
             const cf* tin = keep_t ? ht(it) : spec[cur];
-            if (int e = pass_b_oop(H, tin, spec[cur], fcT, mT, twH, N, (int)P, 0, s)) return e;
+            if (int e = pass_b_oop(H, tin, spec[cur], fcT, mT, twH, N, (int)P, 0, s, (int)Pm)) return e;
         }
         if (it == d.maxit) {
             ProfScope ps(3, s);
@@ -729,21 +748,25 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
             ProfScope ps(2, s);
             float* nout = train ? hn(it) : at<float>(ws, Lo.nsq);
             IsoArgs ia{spec[cur], uxi, uyi, nprev, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
-                       (long long)Lo.ngroups * H};
+                       (long long)Lo.ngroups * H, Pm};
             int e = with_row(N, [&](auto ops) { return decltype(ops)::iso_norm(ia, first, train, s); });
             if (e) return e;
             const long long n4 = 2LL * H * W / 4;
-            hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                               at<float4>(ws, Lo.part), reinterpret_cast<float4*>(nout), Lo.ngroups, n4);
-            if ((e = launch_check("k_iso_reduce"))) return e;
+            const int gpm = Lo.ngroups / G;  // plane groups per module
+            for (int g = 0; g < G; ++g) {     // each module's norm over its own planes
+                hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                                   at<float4>(ws, Lo.part) + (size_t)g * gpm * n4,  // n4 float4 = 2HW floats
+                                   reinterpret_cast<float4*>(nout) + (size_t)g * n4, gpm, n4);
+                if ((e = launch_check("k_iso_reduce"))) return e;
+            }
             // sharded batch: the per-pixel sums must cover every rank's planes
-            if (g_allreduce.fn) g_allreduce.fn(nout, 2ull * H * W, s, g_allreduce.ctx);
+            if (g_allreduce.fn) g_allreduce.fn(nout, (size_t)G * 2 * H * W, s, g_allreduce.ctx);
             nsq = nout;
         }
         {
             ProfScope ps(0, s);
             cf* tout = (keep_t && it < d.maxit) ? ht(it + 1) : spec[1 - cur];
-            PassAArgs pa{spec[cur], tout, bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, rows / R};
+            PassAArgs pa{spec[cur], tout, bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, rows / R, Pm};
             int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, train, s); });
             if (e) return e;
         }
@@ -763,7 +786,8 @@ struct BwdLayout {
 BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     BwdLayout B{};
     B.f = make_layout(d);
-    const size_t img = (size_t)d.B * d.C * d.H * d.W * sizeof(float);
+    const size_t G = ngroups_of(d);
+    const size_t img = G * d.B * d.C * d.H * d.W * sizeof(float);  // all modules' planes
     size_t o = B.f.total;
     auto take = [&](size_t bytes) {
         size_t at_ = o;
@@ -771,8 +795,8 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
         return at_;
     };
     for (int i = 0; i < 4; ++i) B.abar[i] = take(img);
-    B.bbar = take(img);
-    const long long rows = d.B * d.C * d.H;
+    B.bbar = take(img);  // per module; summed into gxin at the end
+    const long long rows = (long long)G * d.B * d.C * d.H;
     if (B.f.gen) {  // generic backward: one partial pair per 256-pixel block
         B.R = 0;
         B.nstrips = (rows * d.W + 255) / 256;
@@ -782,8 +806,8 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     }
     B.part = take((size_t)std::max(d.maxit, 1) * B.nstrips * 2 * sizeof(float));
     B.ntp = 256;
-    B.tpart = take((size_t)std::max(d.maxit, 1) * B.ntp * sizeof(float));
-    B.q = take(2 * (size_t)d.H * d.W * sizeof(float));
+    B.tpart = take((size_t)std::max(d.maxit, 1) * G * B.ntp * sizeof(float));  // [K][G][ntp]
+    B.q = take(G * 2 * (size_t)d.H * d.W * sizeof(float));
     if (d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) {
         const size_t nf = ((size_t)d.W / 2 + 1) * d.H;
         B.xppg = 8;
@@ -883,8 +907,8 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xi
         ain = 1 - ain;
     }
     if (glam && grho) {
-        hipLaunchKernelGGL(k_bwd_scalars, dim3(1), dim3(256), 0, s, part, (long long)K * BL.nstrips, tpart,
-                           d.iso ? K * BL.ntp : 0, lam, rho, glam, grho);
+        hipLaunchKernelGGL(k_bwd_scalars, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, BL.nstrips, 0LL,
+                           d.iso ? tpart : nullptr, BL.ntp, 1, 0, lam, rho, glam, grho);
         if (int e = launch_check("k_bwd_scalars")) return e;
     } else if (glam || grho) {
         return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
@@ -966,16 +990,17 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     const Layout& Lo = BL.f;
     if (!ws || ws_bytes < BL.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
         return fail(ADMM_TV_EWORKSPACE, "workspace too small or not 256-byte aligned");
-    const long long P = d.B * d.C;
+    const int G = ngroups_of(d);
+    const long long Pm = d.B * d.C, P = G * Pm;  // planes of one module, of all modules
     const int H = (int)d.H, W = (int)d.W, N = W / 2, K = d.maxit;
-    const size_t img_bytes = (size_t)P * H * W * sizeof(float);
+    const size_t img_bytes = (size_t)Pm * H * W * sizeof(float);  // gxin: one module's planes
     const bool psf_grad = gkern != nullptr;
     if (psf_grad && (d.kh == 0 || !(d.flags & ADMM_TV_FLAG_PSF_GRAD) || !xin))
         return fail(ADMM_TV_EINVAL, "gkern needs a PSF, ADMM_TV_FLAG_PSF_GRAD (forward and backward) and xin");
     if (K == 0) {  // output is identically zero
         if (gxin) HIPCHK(hipMemsetAsync(gxin, 0, img_bytes, s));
-        if (glam) HIPCHK(hipMemsetAsync(glam, 0, sizeof(float), s));
-        if (grho) HIPCHK(hipMemsetAsync(grho, 0, sizeof(float), s));
+        if (glam) HIPCHK(hipMemsetAsync(glam, 0, sizeof(float) * G, s));
+        if (grho) HIPCHK(hipMemsetAsync(grho, 0, sizeof(float) * G, s));
         if (gkern) HIPCHK(hipMemsetAsync(gkern, 0, sizeof(float) * d.kh * d.kw, s));
         return 0;
     }
@@ -1001,13 +1026,13 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     cf* spec[2] = {at<cf>(ws, Lo.spec[0]), at<cf>(ws, Lo.spec[1])};
     float* ab[4] = {at<float>(ws, BL.abar[0]), at<float>(ws, BL.abar[1]), at<float>(ws, BL.abar[2]),
                     at<float>(ws, BL.abar[3])};
-    // b^ accumulates straight into gxin when there is no PSF (x^_in = b^)
-    float* bbar = (d.kh == 0 && gxin) ? gxin : at<float>(ws, BL.bbar);
+    // b^ accumulates straight into gxin when there is no PSF and one module (x^_in = b^)
+    float* bbar = (d.kh == 0 && gxin && G == 1) ? gxin : at<float>(ws, BL.bbar);
     float* part = at<float>(ws, BL.part);
     float* tpart = at<float>(ws, BL.tpart);
     float* q = at<float>(ws, BL.q);
     const long long rows = P * H;
-    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * BL.ntp * sizeof(float), s));
+    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * G * BL.ntp * sizeof(float), s));
     int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(gout, spec[0], twW, rows, s); });
     if (e) return e;
     int cur = 0, ain = 0;
@@ -1020,24 +1045,30 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
         }
         {
             ProfScope ps(1, s);
-            if ((e = pass_b(H, spec[cur], fcT, mT, twH, N, (int)P, 0, s))) return e;
+            if ((e = pass_b(H, spec[cur], fcT, mT, twH, N, (int)P, 0, s, (int)Pm))) return e;
         }
         const bool lastk = (k == K), firstk = (k == 1);
         if (d.iso && !firstk) {
             ProfScope ps(2, s);
             BwdIsoArgs qa{spec[cur], ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0), ha(k - 1, 1), rho,
-                          at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg, (long long)Lo.ngroups * H};
+                          at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg, (long long)Lo.ngroups * H, Pm};
             if ((e = with_row(N, [&](auto ops) { return decltype(ops)::bwd_iso_q(qa, lastk, s); }))) return e;
             const long long n4 = 2LL * H * W / 4;
-            hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                               at<float4>(ws, Lo.part), reinterpret_cast<float4*>(q), Lo.ngroups, n4);
-            if ((e = launch_check("k_iso_reduce"))) return e;
-            // tau^ partial from this rank's Q (the norm N is already global): summing the
-            // ranks' lambda/rho gradients then counts every plane once
-            hipLaunchKernelGGL(k_iso_tau_partial, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
-                               tpart + (size_t)(K - k) * BL.ntp, 2LL * H * W);
-            if ((e = launch_check("k_iso_tau_partial"))) return e;
-            if (g_allreduce.fn) g_allreduce.fn(q, 2ull * H * W, s, g_allreduce.ctx);
+            const int gpm = Lo.ngroups / G;
+            for (int g = 0; g < G; ++g) {  // per module: Q over its planes, then its tau^ partial
+                float* qg = q + (size_t)g * 2 * H * W;
+                hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                                   at<float4>(ws, Lo.part) + (size_t)g * gpm * n4, reinterpret_cast<float4*>(qg),
+                                   gpm, n4);
+                if ((e = launch_check("k_iso_reduce"))) return e;
+                // tau^ partial from this rank's Q (the norm N is already global): summing the
+                // ranks' lambda/rho gradients then counts every plane once
+                hipLaunchKernelGGL(k_iso_tau_partial, dim3(BL.ntp), dim3(256), 0, s, qg,
+                                   hn(k - 1) + (size_t)g * 2 * H * W, lam + g, rho + g,
+                                   tpart + ((size_t)(K - k) * G + g) * BL.ntp, 2LL * H * W);
+                if ((e = launch_check("k_iso_tau_partial"))) return e;
+            }
+            if (g_allreduce.fn) g_allreduce.fn(q, (size_t)G * 2 * H * W, s, g_allreduce.ctx);
         }
         {
             ProfScope ps(0, s);
@@ -1046,7 +1077,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
                        ha(k, 0), ha(k, 1),
                        firstk ? nullptr : ha(k - 1, 0), firstk ? nullptr : ha(k - 1, 1),
                        (d.iso && !firstk) ? hn(k - 1) : nullptr, q, lam, rho,
-                       part + (size_t)(K - k) * BL.nstrips * 2, twW, H, BL.R, BL.nstrips};
+                       part + (size_t)(K - k) * BL.nstrips * 2, twW, H, BL.R, BL.nstrips, Pm};
             if ((e = with_row(N, [&](auto ops) { return decltype(ops)::bwd_pass_a(ba, d.iso != 0, lastk, firstk, s); })))
                 return e;
         }
@@ -1054,9 +1085,12 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
         ain = 1 - ain;
     }
     if (glam && grho) {
-        hipLaunchKernelGGL(k_bwd_scalars, dim3(1), dim3(256), 0, s, part, (long long)K * BL.nstrips, tpart,
-                           d.iso ? K * BL.ntp : 0, lam, rho, glam, grho);
-        if ((e = launch_check("k_bwd_scalars"))) return e;
+        const long long spm = BL.nstrips / G;  // strips of one module (module-major planes)
+        for (int g = 0; g < G; ++g) {
+            hipLaunchKernelGGL(k_bwd_scalars, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, spm, (long long)g * spm,
+                               d.iso ? tpart : nullptr, BL.ntp, G, g, lam + g, rho + g, glam + g, grho + g);
+            if ((e = launch_check("k_bwd_scalars"))) return e;
+        }
     } else if (glam || grho) {
         return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
     }
@@ -1070,6 +1104,13 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
         hipLaunchKernelGGL(k_psf_grad, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
                            at<double2>(ws, BL.zacc), at<double2>(ws, Lo.sigma), d.kh, H, W, gkern, 0.25);
         if ((e = launch_check("k_psf_grad"))) return e;
+    }
+    if (gxin && G > 1) {  // the modules share xin: x^_in collects every module's b^
+        const long long n4 = Pm * H * W / 4;
+        float* sum = d.kh > 0 ? bbar : gxin;  // with a PSF, sum in place (module 0's slot) first
+        hipLaunchKernelGGL(k_sum_modules, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                           reinterpret_cast<const float4*>(bbar), reinterpret_cast<float4*>(sum), G, n4);
+        if ((e = launch_check("k_sum_modules"))) return e;
     }
     if (gxin && d.kh > 0) {
         // x^_in = H_t^T b^ : the conjugate multiplier (pass B mode 2)

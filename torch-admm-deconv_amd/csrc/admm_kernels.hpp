@@ -256,7 +256,7 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
 template <int H, int C, int MODE>
 __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCfg<H>::E), sizeof(cf) * (H + (size_t)H * C)))
     k_pass_b(const cf* spec_in, cf* spec_out, const float* __restrict__ fcT, const cf* __restrict__ mT,
-             const cf* __restrict__ twH_g, int N, int colblocks) {
+             const cf* __restrict__ twH_g, int N, int colblocks, int ppm) {
     using G = ColGeom<H, C>;
     constexpr int E = G::E, L = G::L;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -268,6 +268,7 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
     const int p = lb / colblocks, cb = lb % colblocks;
     const int col = cb * C + c;
+    if (MODE == 0) fcT += (size_t)(p / ppm) * (N + 1) * H;  // this module's Wiener factor
     // one plane of the spectrum = H*N*8 bytes (< 4 GiB); element (row, col) at (row*N + col)*8
     const rsrc_t rs = make_rsrc(spec_in + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
     const rsrc_t ro = make_rsrc(spec_out + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
@@ -346,7 +347,7 @@ __device__ __forceinline__ void bstore_f4(rsrc_t r, int voff, int soff, float4 v
 template <int H, int CP>
 __global__ void __launch_bounds__(CP * (H / RowCfg<H>::E), PASSB2_MINW)
     k_pass_b2(const cf* spec_in, cf* spec_out, const float* __restrict__ fcT, const cf* __restrict__ twH_g, int N,
-              int colblocks) {
+              int colblocks, int ppm) {
     using G = ColGeom<H, CP>;
     constexpr int E = G::E, L = G::L;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -358,6 +359,7 @@ __global__ void __launch_bounds__(CP * (H / RowCfg<H>::E), PASSB2_MINW)
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
     const int p = lb / colblocks, cb = lb % colblocks;
     const int col = cb * 2 * CP + 2 * cp;  // this thread's columns: col, col + 1
+    fcT += (size_t)(p / ppm) * (N + 1) * H;  // this module's Wiener factor
     const rsrc_t rs = make_rsrc(spec_in + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
     const rsrc_t ro = make_rsrc(spec_out + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
     const int voff = (t * N + col) * (int)sizeof(cf);
@@ -435,6 +437,9 @@ struct PassAArgs {
     int H;
     int R;                // rows per strip (divides H)
     long long nstrips;
+    long long ppm;        // planes per module: with several modules solved together (desc.groups),
+                          // module m = plane / ppm has lam[m], rho[m], norms at nsq + m 2HW, and
+                          // all modules share b (b has ppm planes)
 };
 
 // occupancy target of the row pass (waves per SIMD): 3 for rows up to W = 1024 (fits
@@ -484,21 +489,23 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
     const long long p = strip / spp;
     const int i0 = (int)(strip % spp) * R;
     RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
-    const float rho = a.rho[0];
-    const float tau = a.lam[0] / rho;
+    const int mod = (int)(p / a.ppm);
+    const float rho = a.rho[mod];
+    const float tau = a.lam[mod] / rho;
 
     const cf* sp = a.sin + (size_t)p * H * N;
     cf* so = a.sout + (size_t)p * H * N;
     const size_t poff = (size_t)p * H * W;
-    const cf* bimg = reinterpret_cast<const cf*>(a.b + poff);
+    const cf* bimg = reinterpret_cast<const cf*>(a.b + (size_t)(p - (long long)mod * a.ppm) * H * W);
     const cf* uxi = reinterpret_cast<const cf*>(a.uxi + poff);
     const cf* uyi = reinterpret_cast<const cf*>(a.uyi + poff);
     cf* uxo = reinterpret_cast<cf*>(a.uxo + poff);
     cf* uyo = reinterpret_cast<cf*>(a.uyo + poff);
-    const cf* nsx = reinterpret_cast<const cf*>(a.nsq);
-    const cf* nsy = reinterpret_cast<const cf*>(a.nsq + (size_t)H * W);
-    const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev);
-    const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + (size_t)H * W);
+    const size_t moff = (size_t)mod * 2 * H * W;  // this module's norm maps
+    const cf* nsx = reinterpret_cast<const cf*>(a.nsq + moff);
+    const cf* nsy = reinterpret_cast<const cf*>(a.nsq + moff + (size_t)H * W);
+    const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev + moff);
+    const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + moff + (size_t)H * W);
 
     // Loads are issued ahead of the transforms that precede their use (PASSA_PF): the LDS
     // fences inside the FFTs keep the compiler from hoisting them itself, so without this
@@ -651,8 +658,9 @@ struct IsoArgs {
     const float* rho;
     float* partial;  // [ngroups][2][H][W]
     const cf* twW;
-    int P, H, ppg;   // planes per group
+    int P, H, ppg;   // planes per group (a plane group never straddles two modules)
     long long nitems;  // ngroups * H
+    long long ppm;     // planes per module (see PassAArgs)
 };
 
 template <int N, bool FIRST, bool HIST>
@@ -671,9 +679,11 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
     const int grp = (int)(item / H);
     const int gm = (g - 1 + H) & (H - 1);
     RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
-    const float tau = HIST ? a.lam[0] / a.rho[0] : 0.f;
-    const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev);
-    const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + (size_t)H * W);
+    const int mod = (int)((long long)grp * a.ppg / a.ppm);
+    const float tau = HIST ? a.lam[mod] / a.rho[mod] : 0.f;
+    const size_t moff = (size_t)mod * 2 * H * W;
+    const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev + moff);
+    const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + moff + (size_t)H * W);
     cf sx[E], sy[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) sx[j] = sy[j] = mkc(0.f, 0.f);
