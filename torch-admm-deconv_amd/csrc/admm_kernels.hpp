@@ -448,9 +448,6 @@ struct PassAArgs {
 #define PASSA_MINW_SMALL 3
 #endif
 #define PASSA_MINW(n) ((n) >= 1024 ? 1 : PASSA_MINW_SMALL)
-#ifndef PASSA_PF
-#define PASSA_PF 0
-#endif
 
 template <bool ISO> __device__ __forceinline__ float shrink_z(float a, float tau, float nsum) {
     if constexpr (ISO) return block_factor(nsum, tau) * a;
@@ -507,73 +504,28 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
     const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev + moff);
     const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + moff + (size_t)H * W);
 
-    // Loads are issued ahead of the transforms that precede their use (PASSA_PF): the LDS
-    // fences inside the FFTs keep the compiler from hoisting them itself, so without this
-    // every load group waits a full HBM round trip right before it is consumed.
-    //   PF >= 1: the next row's spectrum is loaded while the current row is processed
-    //   PF >= 2: u_y / u_x of the current row are loaded before its c2r
-    //   PF >= 3: b of the row being finalised is loaded before the c2r
-    constexpr int PF = PASSA_PF;
-    cf xprev[E], xcur[E], wxp[E], wyp[E], xnext[E];
+    cf xprev[E], xcur[E], wxp[E], wyp[E];
     {
         const int g = (i0 - 1 + H) & (H - 1);
 #pragma unroll
         for (int j = 0; j < E; ++j) xprev[j] = sp[(size_t)g * N + t + L * j];
-        if constexpr (PF >= 1) {
-#pragma unroll
-            for (int j = 0; j < E; ++j) xnext[j] = sp[(size_t)(i0 & (H - 1)) * N + t + L * j];
-        }
         RowXf<N>::c2r(xprev, buf, tw, t);
     }
     for (int rr = 0; rr <= R; ++rr) {
         const int g = (i0 + rr) & (H - 1);
         const size_t ro = (size_t)g * N;  // row offset in cf units (spectrum and pixel pairs alike)
-        const int gm = (g - 1 + H) & (H - 1);
-        const size_t rm = (size_t)gm * N;
-        if constexpr (PF >= 1) {
 #pragma unroll
-            for (int j = 0; j < E; ++j) xcur[j] = xnext[j];
-            if (rr < R) {
-                const size_t rn = (size_t)((g + 1) & (H - 1)) * N;
-#pragma unroll
-                for (int j = 0; j < E; ++j) xnext[j] = sp[rn + t + L * j];
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < E; ++j) xcur[j] = sp[ro + t + L * j];
-        }
-        cf uy[E], fy[E], ux[E], fx[E], bb[E];
-        if constexpr (PF >= 2) {
-#pragma unroll
-            for (int j = 0; j < E; ++j) {
-                uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
-                if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
-            }
-            if (rr < R) {
-#pragma unroll
-                for (int j = 0; j < E; ++j) {
-                    ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
-                    if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
-                }
-            }
-        }
-        if constexpr (PF >= 3) {
-            if (rr >= 1) {
-#pragma unroll
-                for (int j = 0; j < E; ++j) bb[j] = bimg[rm + t + L * j];
-            }
-        }
+        for (int j = 0; j < E; ++j) xcur[j] = sp[ro + t + L * j];
         RowXf<N>::c2r(xcur, buf, tw, t);
 
         // ---- y direction: a_y = x[g] - x[g-1] + u_y; z_y, u_y, w_y of row g
         cf wyc[E];
         {
-            if constexpr (PF < 2) {
+            cf uy[E], fy[E];
 #pragma unroll
-                for (int j = 0; j < E; ++j) {
-                    uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
-                    if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
-                }
+            for (int j = 0; j < E; ++j) {
+                uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
+                if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
             }
 #pragma unroll
             for (int j = 0; j < E; ++j) {
@@ -593,19 +545,18 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
 
         // ---- finalize row g-1: v = Dx^T w_x + Dy^T w_y, r = b + rho v, row FFT
         if (rr >= 1) {
+            const int gm = (g - 1 + H) & (H - 1);
+            const size_t rm = (size_t)gm * N;
             cf r[E], sh[E];
-            if constexpr (PF < 3) {
-#pragma unroll
-                for (int j = 0; j < E; ++j) bb[j] = bimg[rm + t + L * j];
-            }
 #pragma unroll
             for (int j = 0; j < E; ++j) sh[j].x = __shfl(wxp[j].x, (t + 1) & (L - 1), L);
 #pragma unroll
             for (int j = 0; j < E; ++j) {
                 const float wr = (t == L - 1) ? sh[(j + 1) & (E - 1)].x : sh[j].x;  // w_x at pixel q1+1
+                const cf bb = bimg[rm + t + L * j];
                 const float v0 = (wxp[j].x - wxp[j].y) + (wyp[j].x - wyc[j].x);
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
-                r[j] = mkc(fmaf(rho, v0, bb[j].x), fmaf(rho, v1, bb[j].y));
+                r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
             }
             RowXf<N>::r2c(r, buf, tw, t);
 #pragma unroll
@@ -614,13 +565,11 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
 
         // ---- x direction: a_x = x[g][j] - x[g][j-1] + u_x; z_x, u_x, w_x of row g
         if (rr < R) {
-            cf sh[E];
+            cf ux[E], fx[E], sh[E];
 #pragma unroll
             for (int j = 0; j < E; ++j) {
-                if constexpr (PF < 2) {
-                    ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
-                    if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
-                }
+                ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
+                if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
                 sh[j].x = __shfl(xcur[j].y, (t - 1) & (L - 1), L);
             }
 #pragma unroll
