@@ -79,6 +79,7 @@ def test_sharded_world2_on_gpu(cuda_dev, iso):
     for rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat in sorted(q.get(timeout=10) for _ in range(2)):
         print("iso" if iso else "aniso", rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat)
         if iso:
-            assert e_out <= 1e-6 and e_gx <= 1e-5 and e_gl <= 1e-5 and e_gr <= 1e-4 and e_gat <= 1e-6
+            # fp32 reassociation only: per-pixel norms and tau^ partials summed per rank, then across
+            assert e_out <= 1e-6 and e_gx <= 1e-5 and e_gl <= 5e-5 and e_gr <= 1e-4 and e_gat <= 1e-6
         else:
             assert bitexact and e_out == 0.0 and e_gx <= 1e-6 and e_gl <= 1e-5 and e_gr <= 1e-5

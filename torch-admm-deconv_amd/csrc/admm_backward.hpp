@@ -64,8 +64,13 @@ __device__ __forceinline__ float soft_dtau(float a, float zb, float tau) {
     return (fabsf(a) > tau) ? (a > 0.f ? -zb : zb) : 0.f;  // -sign(a) z^ on the active set
 }
 
+// occupancy target of the reverse row pass (waves per SIMD), as PASSA_MINW for the forward:
+// 3 for aniso (measured -2.4 % at C3 size; a few registers spill), 2 for iso, whose extra
+// norm / Q operands would spill ~240 B at 3 (measured +4 %)
+#define BWDA_MINW(n, iso) ((n) >= 1024 ? 1 : (iso) ? 2 : 3)
+
 template <int N, bool ISO, bool LASTK, bool FIRSTK>
-__global__ void __launch_bounds__(256) k_bwd_pass_a(BwdArgs a) {
+__global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a) {
     using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -90,6 +90,11 @@ bool generic_hw(int64_t H, int64_t W) {
     return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax;
 }
 
+int env_int(const char* name, int dflt) {
+    const char* s = std::getenv(name);
+    return s ? std::atoi(s) : dflt;
+}
+
 // modules solved together (admm_tv_desc.groups)
 int ngroups_of(const admm_tv_desc& d) { return d.groups > 1 ? d.groups : 1; }
 
@@ -131,11 +136,17 @@ Layout make_layout(const admm_tv_desc& d) {
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
         // plane groups for the iso norm pass: enough (group,row) items to fill the chip
-        int ppg = 8;
-        if ((size_t)P <= 8) ppg = (int)P;
+        // planes per group: at most 8 (each group writes and the reduce reads one 2HW partial),
+        // fewer when (group, row) items would not give ~3 waves per SIMD (C5: 48 planes of 512^2
+        // -> 4, iso norm -30 %)
+        const int lanes = (int)std::min<size_t>(64, N / (N >= 1024 ? 16 : N >= 64 ? 8 : N >= 16 ? 4 : 2));
+        const long long want = 3LL * 1024 * 64 / std::max(lanes, 1);
+        int ppg = (int)std::max<long long>(1, std::min<long long>(8, (long long)(P * H) / want));
+        ppg = env_int("ADMM_ISO_PPG", ppg);
+        if ((size_t)P <= (size_t)ppg) ppg = (int)P;
         if (G > 1) {  // a plane group must not straddle two modules: a divisor of B*C
             const int pm = (int)(d.B * d.C);
-            ppg = std::min(8, pm);
+            ppg = std::min(ppg, pm);
             while (pm % ppg) --ppg;
         }
         L.ppg = ppg;
@@ -147,10 +158,6 @@ Layout make_layout(const admm_tv_desc& d) {
     return L;
 }
 
-int env_int(const char* name, int dflt) {
-    const char* s = std::getenv(name);
-    return s ? std::atoi(s) : dflt;
-}
 
 template <class T> T* at(void* ws, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(ws) + off); }
 
