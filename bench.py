@@ -39,6 +39,8 @@ CONFIGS = {
                "C3 at 100 iters (SURVEY §8 d1): batch-64 1024x1024x3, 21x21 Gaussian PSF, aniso"),
     "c3iso": (64, 3, 1024, 1024, "gauss:3", 21, 50, True,
               "C3 with block (iso) shrinkage, the ADMMDeconv default: batch-64 1024x1024x3, 21x21 PSF, 50 iters"),
+    "bsd": (32, 3, 321, 481, "gauss:1.5", 9, 50, False,
+            "generic-size path (row f4): batch-32 481x321x3 (BSD image size), 9x9 Gaussian PSF, aniso, 50 iters"),
     "c2": (32, 3, 512, 512, "motion", 15, 50, False,
            "C2: batch-32 512x512x3, 15x15 motion PSF, lambda 0.01, rho 0.02, aniso, 50 iters"),
     "c5fwd": (16, 3, 512, 512, "none", 0, 100, True,

@@ -462,10 +462,13 @@ GPlan make_plan(int n) {
     return p;
 }
 
-// rows per block of the row transforms / columns per block of the column pass, sized so the
-// LDS image (twiddles + two ping-pong buffers) stays within 96 KB
-int grow_lines(int W) { return std::max(1, std::min(32, (12288 / W - 1) / 2)); }
-int gcol_cols(int H) { return std::max(1, std::min(16, (12288 / H - 1) / 2)); }
+// rows per block of the row transforms / columns per block of the column pass
+// (powers of two, so the per-item line index is a shift)
+int pow2_floor(int v) { int p = 1; while (2 * p <= v) p *= 2; return p; }
+// LDS image <= ~32 KB (4+ resident blocks per CU: the prime-radix stages are latency-bound
+// chains and need the waves), except where one line alone is bigger
+int grow_lines(int W) { return pow2_floor(std::max(1, std::min(32, (4096 / W - 1) / 2))); }
+int gcol_cols(int H) { return pow2_floor(std::max(1, std::min(16, (4096 / H - 1) / 2))); }
 
 int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hipStream_t s) {
     GRowArgs a{img, spec, nullptr, tw, make_plan(W), rows, grow_lines(W)};

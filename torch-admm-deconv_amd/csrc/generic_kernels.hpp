@@ -93,7 +93,8 @@ __device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restr
     }
 }
 
-// any radix R: one output element per item, O(R) work
+// any radix R: one output element per item, O(R) work.  The twiddle exponent q (m + k NS) mod
+// (NS R) is stepped incrementally (no integer modulo in the inner loop).
 template <int DIR>
 __device__ __forceinline__ void gstage_any(const cf* __restrict__ src, cf* __restrict__ dst, int n, int NS, int R,
                                            int lines, const cf* __restrict__ tw) {
@@ -104,13 +105,26 @@ __device__ __forceinline__ void gstage_any(const cf* __restrict__ src, cf* __res
         const int c = item % lines, o = item / lines;  // o = vt-major output slot (vt, k)
         const int vt = o % nb, k = o / nb;
         const int m = vt % NS;
-        const int e = m + k * NS;  // exponent base: W_{NS R}^{q (m + k NS)}
-        cf acc = src[vt * lines + c];
-        for (int q = 1; q < R; ++q) {
-            const cf w = twid<DIR>(tw, ((q * e) % span) * tstride);
-            acc = cadd(acc, cmul(src[(vt + q * nb) * lines + c], w));
+        const int e = m + k * NS;  // exponent step: W_{NS R}^{q e}
+        const cf* col = src + vt * lines + c;
+        const int qstep = nb * lines;
+        // two interleaved accumulators (even / odd q) halve the dependent chain
+        cf acc0 = col[0], acc1 = mkc(0.f, 0.f);
+        int idx = e >= span ? e - span : e;  // q = 1
+        const int e2 = (2 * e) % span;
+        int idx2 = idx + e;
+        if (idx2 >= span) idx2 -= span;      // q = 2
+        int q = 1;
+        for (; q + 1 < R; q += 2) {
+            acc1 = cadd(acc1, cmul(col[q * qstep], twid<DIR>(tw, idx * tstride)));
+            acc0 = cadd(acc0, cmul(col[(q + 1) * qstep], twid<DIR>(tw, idx2 * tstride)));
+            idx += e2;
+            if (idx >= span) idx -= span;
+            idx2 += e2;
+            if (idx2 >= span) idx2 -= span;
         }
-        dst[((vt / NS) * span + m + k * NS) * lines + c] = acc;
+        if (q < R) acc1 = cadd(acc1, cmul(col[q * qstep], twid<DIR>(tw, idx * tstride)));
+        dst[((vt / NS) * span + m + k * NS) * lines + c] = cadd(acc0, acc1);
     }
 }
 
