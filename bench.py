@@ -210,8 +210,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # rehearsal on a 1-GPU box (never set by the driver): every rank on cuda:0 over gloo
+        if os.environ.get("ADMM_BENCH_REHEARSAL"):
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if os.environ.get("ADMM_BENCH_REHEARSAL") else "nccl")
     dev = torch.device("cuda", local)
     if args.config == "c5":
         run_c5(args, world, rank, dev)
