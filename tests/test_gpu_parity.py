@@ -184,3 +184,17 @@ def test_c3_full_size_sampled(cuda_dev):
         e = rel(out[b:b + 1, c:c + 1], ref)
         print("C3 plane", b, c, e)
         assert e <= TOL_REF64
+
+
+def test_empty_batch_and_argument_forms(cuda_dev):
+    """Reference argument forms: empty batch -> empty result; lmbd / rho as floats, 1-element
+    tensors (on the device or the host); negative maxit -> zeros; integer iso; float maxit."""
+    from admmtor.eops.deconv import fft_admm_tv
+    x = torch.rand(0, 3, 32, 32, device=cuda_dev)
+    assert fft_admm_tv(x, 0.01, 0.02, torch.empty(0, device=cuda_dev), False, 5).shape == (0, 3, 32, 32)
+    x = torch.rand(1, 2, 32, 32, device=cuda_dev)
+    k = torch.ones(1, 1, 3, 3, device=cuda_dev) / 9
+    a = fft_admm_tv(x, 0.01, 0.02, k, False, 5)
+    b = fft_admm_tv(x, torch.tensor([0.01]), torch.tensor(0.02, device=cuda_dev), k, 0, 5.0)
+    assert torch.equal(a, b)
+    assert torch.count_nonzero(fft_admm_tv(x, 0.01, 0.02, k, False, -3)).item() == 0

@@ -157,6 +157,8 @@ def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> 
         raise RuntimeError("admmtor (MI355X build): fft_admm_tv runs on ROCm device tensors only; "
                            "move xin (and kern) to the GPU. There is no CPU path.")
     maxit = max(0, int(maxit))  # the reference loops over torch.arange(0, maxit): negative -> no iteration
+    if xin.numel() == 0:  # empty batch: the reference's ops return an empty result of the same shape
+        return torch.zeros(xin.shape, dtype=torch.float32, device=xin.device)
     dev = xin.device
     x32 = xin.detach().to(torch.float32).contiguous()
     k32 = kern.detach().to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \
