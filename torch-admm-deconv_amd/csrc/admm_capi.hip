@@ -462,7 +462,8 @@ GPlan make_plan(int n) {
     return p;
 }
 
-// rows per block of the row transforms / columns per block of the column pass
+// complex rows (= 2 real rows each) per block of the row transforms / columns per block of
+// the column pass
 // (powers of two, so the per-item line index is a shift)
 int pow2_floor(int v) { int p = 1; while (2 * p <= v) p *= 2; return p; }
 // LDS image <= ~32 KB (4+ resident blocks per CU: the prime-radix stages are latency-bound
@@ -474,14 +475,14 @@ int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hi
     GRowArgs a{img, spec, nullptr, tw, make_plan(W), rows, grow_lines(W)};
     const size_t lds = sizeof(cf) * (size_t)W * (1 + 2 * a.lines);
     if (int e = set_lds(k_grow_fwd, lds)) return e;
-    hipLaunchKernelGGL(k_grow_fwd, dim3((unsigned)((rows + a.lines - 1) / a.lines)), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(k_grow_fwd, dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
     return launch_check("k_grow_fwd");
 }
 int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hipStream_t s) {
     GRowArgs a{nullptr, const_cast<cf*>(spec), img, tw, make_plan(W), rows, grow_lines(W)};
     const size_t lds = sizeof(cf) * (size_t)W * (1 + 2 * a.lines);
     if (int e = set_lds(k_grow_inv, lds)) return e;
-    hipLaunchKernelGGL(k_grow_inv, dim3((unsigned)((rows + a.lines - 1) / a.lines)), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(k_grow_inv, dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
     return launch_check("k_grow_inv");
 }
 int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H, int W, long long P, int mode,

@@ -166,6 +166,9 @@ struct GRowArgs {
     int lines;         // rows per block
 };
 
+// Real rows are transformed two at a time: rows a, b as one complex row z = a + i b, whose
+// spectrum Z gives A[k] = (Z[k] + conj Z[-k]) / 2 and B[k] = (Z[k] - conj Z[-k]) / 2i.  A block
+// holds `lines` complex rows = 2 * lines real rows.
 __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
@@ -173,17 +176,23 @@ __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
     cf* A = tw + W;
     cf* B = A + (size_t)W * lines;
     for (int i = threadIdx.x; i < W; i += blockDim.x) tw[i] = a.tw[i];
-    const long long r0 = (long long)blockIdx.x * lines;
-    const int nl = (int)min((long long)lines, a.rows - r0);
-    for (int idx = threadIdx.x; idx < W * lines; idx += blockDim.x) {
-        const int c = idx / W, i = idx % W;  // coalesced along the row
-        A[i * lines + c] = mkc(c < nl ? a.img[(r0 + c) * W + i] : 0.f, 0.f);
+    const long long r0 = (long long)blockIdx.x * 2 * lines;
+    const int nl = (int)min((long long)2 * lines, a.rows - r0);  // real rows in this block
+    for (int idx = threadIdx.x; idx < W * 2 * lines; idx += blockDim.x) {
+        const int rr = idx / W, i = idx % W;  // coalesced along the row
+        const float v = rr < nl ? a.img[(r0 + rr) * W + i] : 0.f;
+        float* slot = reinterpret_cast<float*>(&A[i * lines + (rr >> 1)]);
+        slot[rr & 1] = v;  // even row -> real part, odd row -> imaginary part
     }
     __syncthreads();
     const cf* res = gfft_lds<-1>(A, B, a.plan, lines, tw);
     for (int idx = threadIdx.x; idx < Wh * lines; idx += blockDim.x) {
         const int c = idx / Wh, k = idx % Wh;
-        if (c < nl) a.spec[(r0 + c) * Wh + k] = res[k * lines + c];
+        const cf z = res[k * lines + c];
+        const cf m = res[((W - k) % W) * lines + c];
+        const long long ra = r0 + 2 * c;
+        if (2 * c < nl) a.spec[ra * Wh + k] = mkc(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));
+        if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkc(0.5f * (z.y + m.y), 0.5f * (m.x - z.x));
     }
 }
 
@@ -194,28 +203,33 @@ __global__ void __launch_bounds__(256) k_grow_inv(GRowArgs a) {
     cf* A = tw + W;
     cf* B = A + (size_t)W * lines;
     for (int i = threadIdx.x; i < W; i += blockDim.x) tw[i] = a.tw[i];
-    const long long r0 = (long long)blockIdx.x * lines;
-    const int nl = (int)min((long long)lines, a.rows - r0);
+    const long long r0 = (long long)blockIdx.x * 2 * lines;
+    const int nl = (int)min((long long)2 * lines, a.rows - r0);
+    // Hermitian completion of a half spectrum: X[k] = conj X[W - k] for k >= Wh; the imaginary
+    // parts of the self-conjugate bins (DC, and Nyquist for even W) are dropped, as irfft does
+    auto full = [&](long long row, int k) -> cf {
+        if (k < Wh) {
+            cf v = a.spec[row * Wh + k];
+            if (k == 0 || 2 * k == W) v.y = 0.f;
+            return v;
+        }
+        return cconj(a.spec[row * Wh + (W - k)]);
+    };
     for (int idx = threadIdx.x; idx < W * lines; idx += blockDim.x) {
         const int c = idx / W, k = idx % W;
-        cf v = mkc(0.f, 0.f);
-        if (c < nl) {
-            // Hermitian completion: X[k] = conj X[W - k] for k >= Wh; the imaginary parts of
-            // the self-conjugate bins (DC, and Nyquist for even W) are dropped, as irfft does
-            if (k < Wh) {
-                v = a.spec[(r0 + c) * Wh + k];
-                if (k == 0 || 2 * k == W) v.y = 0.f;
-            } else {
-                v = cconj(a.spec[(r0 + c) * Wh + (W - k)]);
-            }
-        }
-        A[k * lines + c] = v;
+        const long long ra = r0 + 2 * c;
+        const cf xa = 2 * c < nl ? full(ra, k) : mkc(0.f, 0.f);
+        const cf xb = 2 * c + 1 < nl ? full(ra + 1, k) : mkc(0.f, 0.f);
+        A[k * lines + c] = mkc(xa.x - xb.y, xa.y + xb.x);  // Z = Xa + i Xb
     }
     __syncthreads();
     const cf* res = gfft_lds<+1>(A, B, a.plan, lines, tw);
-    for (int idx = threadIdx.x; idx < W * lines; idx += blockDim.x) {
-        const int c = idx / W, i = idx % W;
-        if (c < nl) a.img_out[(r0 + c) * W + i] = res[i * lines + c].x;
+    for (int idx = threadIdx.x; idx < W * 2 * lines; idx += blockDim.x) {
+        const int rr = idx / W, i = idx % W;
+        if (rr < nl) {
+            const cf z = res[i * lines + (rr >> 1)];
+            a.img_out[(r0 + rr) * W + i] = (rr & 1) ? z.y : z.x;
+        }
     }
 }
 
