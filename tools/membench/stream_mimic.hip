@@ -269,6 +269,59 @@ __global__ void __launch_bounds__(TPB) k_colmimic(cf* __restrict__ spec, int H, 
     for (int j = 0; j < 32; ++j) if (j < E) { v[j].x *= 1.0001f; base[(size_t)(t + L * j) * N] = v[j]; }
 }
 
+
+// column-tiled spectrum layout [P][H/T][N/8][T][8] (u, b stay row-major): offset of (row, col) in cf units
+template <int T> __device__ __forceinline__ size_t toff(int row, int col) {
+    return ((size_t)(row / T) * (N / 8) + (col >> 3)) * (T * 8) + (row % T) * 8 + (col & 7);
+}
+// pass A mimic with the spectrum streams (sp in, so out) in the tiled layout
+template <int R, int T>
+__global__ void __launch_bounds__(256) k_mimic_t(const cf* __restrict__ sp, const cf* __restrict__ uxi,
+                                                 const cf* __restrict__ uyi, const cf* __restrict__ b,
+                                                 cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
+                                                 int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    cf acc[E];
+    for (int j = 0; j < E; ++j) acc[j] = sp[base + toff<T>((i0 - 1 + H) & (H - 1), t + L * j)];
+    for (int rr = 0; rr <= R; ++rr) {
+        const int gi = (i0 + rr) & (H - 1), gm = (i0 + rr - 1 + H) & (H - 1);
+        const size_t ro = base + (size_t)gi * N;
+        const size_t rm = base + (size_t)gm * N;
+        cf x[E], uy[E];
+        for (int j = 0; j < E; ++j) x[j] = sp[base + toff<T>(gi, t + L * j)];
+        for (int j = 0; j < E; ++j) { uy[j] = uyi[ro + t + L * j]; uy[j].x += x[j].x; uy[j].y += acc[j].y; }
+        if (rr < R) for (int j = 0; j < E; ++j) uyo[ro + t + L * j] = uy[j];
+        if (rr >= 1) {
+            for (int j = 0; j < E; ++j) { cf bb = b[rm + t + L * j]; acc[j].x += bb.x; acc[j].y -= bb.y; }
+            for (int j = 0; j < E; ++j) so[base + toff<T>(gm, t + L * j)] = acc[j];
+        }
+        if (rr < R) {
+            for (int j = 0; j < E; ++j) { cf u = uxi[ro + t + L * j]; u.x -= x[j].y; u.y += x[j].x; uxo[ro + t + L * j] = u; }
+        }
+        for (int j = 0; j < E; ++j) acc[j] = x[j];
+    }
+}
+// pass B mimic on the tiled layout: a block owns 8 adjacent columns (one tile column), all H rows
+template <int TPB, int T>
+__global__ void __launch_bounds__(TPB) k_colmimic_t(cf* __restrict__ spec, int H, int colblocks) {
+    constexpr int C = 8, LL = TPB / C;
+    const int c = threadIdx.x % C, t = threadIdx.x / C;
+    const int p = blockIdx.x / colblocks, cb = blockIdx.x % colblocks;
+    cf* base = spec + (size_t)p * H * N;
+    const int EE = H / LL;
+    cf v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < EE) v[j] = base[toff<T>(t + LL * j, cb * 8 + c)];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < EE) { v[j].x *= 1.0001f; base[toff<T>(t + LL * j, cb * 8 + c)] = v[j]; }
+}
+
 int main() {
     const int P = 192, H = 1024;
     const size_t n = (size_t)P * H * N;  // cf per array
@@ -294,6 +347,60 @@ int main() {
         printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
     const double arr = (double)n * sizeof(cf);
+    if (getenv("TILE_SWEEP")) {
+        const long long ns = (long long)P * H / 8;
+        for (int rep = 0; rep < 2; ++rep) {
+            timeit("A row-major 4R+3W R=8", 7 * arr, [&] { k_mimic<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A tiled T=8 4R+3W R=8", 7 * arr, [&] { k_mimic_t<8, 8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A tiled T=16 4R+3W R=8", 7 * arr, [&] { k_mimic_t<8, 16><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A tiled T=4 4R+3W R=8", 7 * arr, [&] { k_mimic_t<8, 4><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A tiled T=2 4R+3W R=8", 7 * arr, [&] { k_mimic_t<8, 2><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            const int colblocks = N / 8;
+            timeit("B row-major C=8 512thr", 2 * arr, [&] { k_colmimic<8, 512><<<(unsigned)(P * colblocks), 512>>>(buf[0], H, colblocks); });
+            timeit("B row-major C=16 1024thr", 2 * arr, [&] { k_colmimic<16, 1024><<<(unsigned)(P * colblocks / 2), 1024>>>(buf[0], H, colblocks / 2); });
+            timeit("B tiled T=8 C=8 512thr", 2 * arr, [&] { k_colmimic_t<512, 8><<<(unsigned)(P * colblocks), 512>>>(buf[0], H, colblocks); });
+            timeit("B tiled T=16 C=8 512thr", 2 * arr, [&] { k_colmimic_t<512, 16><<<(unsigned)(P * colblocks), 512>>>(buf[0], H, colblocks); });
+            timeit("B tiled T=4 C=8 512thr", 2 * arr, [&] { k_colmimic_t<512, 4><<<(unsigned)(P * colblocks), 512>>>(buf[0], H, colblocks); });
+            timeit("B tiled T=2 C=8 512thr", 2 * arr, [&] { k_colmimic_t<512, 2><<<(unsigned)(P * colblocks), 512>>>(buf[0], H, colblocks); });
+            timeit("copy float4", 2 * arr, [&] { k_copy<false><<<16384, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
+        }
+        return 0;
+    }
+    if (getenv("MALL_SWEEP")) {
+        // one ADMM iteration's traffic pattern (pass A mimic + pass B mimic, ping-ponged spectrum and u)
+        // run ITERS times on a chunk of Pc planes before moving to the next chunk: does a chunk
+        // whose working set fits the 256 MiB Infinity Cache stream faster than HBM?
+        const int ITERS = 50;
+        const int chunks[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 48, 192};
+        for (int rep = 0; rep < 2; ++rep)
+        for (int Pc : chunks) {
+            const size_t pn = (size_t)H * N;  // cf per plane
+            auto run = [&] {
+                for (int p0 = 0; p0 < P; p0 += Pc) {
+                    const int pc = (P - p0 < Pc) ? P - p0 : Pc;
+                    const size_t off = (size_t)p0 * pn;
+                    const long long ns = (long long)pc * H / 8;
+                    for (int it = 0; it < ITERS; ++it) {
+                        cf* si = buf[it & 1 ? 6 : 0] + off; cf* so = buf[it & 1 ? 0 : 6] + off;
+                        cf* xi = buf[it & 1 ? 4 : 1] + off; cf* xo = buf[it & 1 ? 1 : 4] + off;
+                        cf* yi = buf[it & 1 ? 5 : 2] + off; cf* yo = buf[it & 1 ? 2 : 5] + off;
+                        k_mimic<8><<<(unsigned)((ns + 3) / 4), 256>>>(si, xi, yi, buf[3] + off, xo, yo, so, H, ns);
+                        k_colmimic<8, 512><<<(unsigned)(pc * (N / 8)), 512>>>(so, H, N / 8);
+                    }
+                }
+            };
+            run();
+            hipEventRecord(e0);
+            run();
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms; hipEventElapsedTime(&ms, e0, e1);
+            const double bytes = 9.0 * arr * ITERS;  // 36 B/px per iteration = 9 cf-arrays of 8 B per 2 px
+            printf("chunk %3d planes (%6.1f MiB live): %8.2f ms for %d it  -> %6.0f GB/s algorithmic, %6.1f it/s\n",
+                   Pc, Pc * pn * sizeof(cf) * 7 / 1048576.0, ms, ITERS, bytes / (ms * 1e-3) / 1e9, ITERS / (ms * 1e-3));
+        }
+        return 0;
+    }
     if (getenv("AB_ONLY")) {
         const long long ns = (long long)P * H / 8;
         for (int rep = 0; rep < 4; ++rep) {
