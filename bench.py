@@ -167,16 +167,30 @@ def run_c5(args, world, rank, dev):
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
+    if rank == 0:  # heartbeat: the first step (MIOpen kernel searches) can take minutes on a fresh box
+        import threading
+        t_start = time.time()
+
+        def beat():
+            while True:
+                time.sleep(30)
+                print(f"c5 alive {time.time() - t_start:.0f} s", file=sys.stderr, flush=True)
+        threading.Thread(target=beat, daemon=True).start()
+    for i in range(args.warmup):
         step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"c5 warmup step {i + 1}/{args.warmup} done", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     _native.profile_reset()
     _native.profile_enable(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         loss = step()
+        if rank == 0:  # progress for long runs (host-side only: no sync inside the timed region)
+            print(f"c5 step {i + 1}/{args.steps} enqueued", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -2,7 +2,8 @@
 an NCHW tensor, so the fused channel-statistics kernel can follow the same rule."""
 import torch
 
-dev = torch.device("cuda:0")
+import sys
+dev = torch.device(sys.argv[1] if len(sys.argv) > 1 else "cuda:0")
 g = torch.Generator().manual_seed(0)
 for C in (8, 86, 129):
     for dt in (torch.bfloat16, torch.float32):

@@ -37,6 +37,14 @@ EXPORTED = (
     "admm_tv_profile_read",
     "admm_tv_last_error",
 )
+# every symbol include/admm_chanstat.h declares
+EXPORTED_CHANSTAT = (
+    "admm_chanstat_max_channels",
+    "admm_chanstat_pool",
+    "admm_chanstat_pool_depth",
+    "admm_chanstat_pool_backward",
+)
+CHANSTAT_F32, CHANSTAT_BF16, CHANSTAT_F16 = 0, 1, 2
 
 
 class AdmmTvDesc(ctypes.Structure):
@@ -119,6 +127,15 @@ def load() -> ctypes.CDLL:
         L.admm_tv_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
         L.admm_tv_last_error.restype = ctypes.c_char_p
         L.admm_tv_last_error.argtypes = []
+        i64 = ctypes.c_int64
+        L.admm_chanstat_max_channels.restype = ctypes.c_int
+        L.admm_chanstat_max_channels.argtypes = [ctypes.c_int]
+        L.admm_chanstat_pool.restype = ctypes.c_int
+        L.admm_chanstat_pool.argtypes = [ctypes.c_int, vp, i64, i64, i64, vp, vp, vp]
+        L.admm_chanstat_pool_depth.restype = ctypes.c_int
+        L.admm_chanstat_pool_depth.argtypes = [ctypes.c_int, vp, i64, i64, i64, vp, vp, ctypes.c_int, vp]
+        L.admm_chanstat_pool_backward.restype = ctypes.c_int
+        L.admm_chanstat_pool_backward.argtypes = [ctypes.c_int, vp, vp, vp, vp, i64, i64, i64, vp, vp]
         if L.admm_tv_abi_version() != ABI_VERSION:
             raise ImportError("admmtor: native library ABI version mismatch")
         _lib = L

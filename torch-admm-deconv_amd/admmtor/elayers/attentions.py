@@ -7,9 +7,12 @@ Mirrors the module tree and parameter names of
   CBAM.spatial_gate : SpatialGate  (spatial.conv, spatial.norm)          attentions.py:50-60
   BasicConv         : conv -> InstanceNorm2d(affine) -> GELU|Identity    attentions.py:13-33
 
-These are plain PyTorch (GEMM/conv-shaped work goes to MIOpen/hipBLASLt); only
-the ADMM solver on this path is a hand-written kernel.
+These are plain PyTorch (GEMM/conv-shaped work goes to MIOpen/hipBLASLt), except the spatial
+gate's per-pixel channel statistics (ChannelPool), which are one HIP kernel on the GPU
+(include/admm_chanstat.h) -- PyTorch's sort-based mode/median were 46 % of the config-5 step.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -38,15 +41,80 @@ class BasicConv(nn.Module):
         return self.activation(self.norm(self.conv(x)))
 
 
+_CHANSTAT_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def _chanstat_native(x: torch.Tensor, depth_limit=None):
+    """(B, C, H, W) device tensor -> (out (B, 3, H, W), idx (B, 2, H, W) int16) via the HIP kernel of
+    include/admm_chanstat.h; idx holds the channels the median and the mode were taken from."""
+    from .. import _native
+    lib = _native.load()
+    B, C, H, W = x.shape
+    out = torch.empty((B, 3, H, W), dtype=x.dtype, device=x.device)
+    idx = torch.empty((B, 2, H, W), dtype=torch.int16, device=x.device)
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    dt = _CHANSTAT_DTYPES[x.dtype]
+    if depth_limit is None:
+        code = lib.admm_chanstat_pool(dt, x.data_ptr(), B, C, H * W, out.data_ptr(), idx.data_ptr(), stream)
+    else:
+        code = lib.admm_chanstat_pool_depth(dt, x.data_ptr(), B, C, H * W, out.data_ptr(), idx.data_ptr(),
+                                            int(depth_limit), stream)
+    _native.check(code)
+    return out, idx
+
+
+class _ChannelPoolFn(torch.autograd.Function):
+    """ChannelPool's forward and backward as two HIP kernels (include/admm_chanstat.h)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        out, idx = _chanstat_native(x)
+        ctx.save_for_backward(x, out, idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        from .. import _native
+        x, out, idx = ctx.saved_tensors
+        gout = gout.to(x.dtype).contiguous()
+        gx = torch.empty_like(x)
+        B, C, H, W = x.shape
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        _native.check(_native.load().admm_chanstat_pool_backward(
+            _CHANSTAT_DTYPES[x.dtype], x.data_ptr(), out.data_ptr(), idx.data_ptr(), gout.data_ptr(), B, C, H * W,
+            gx.data_ptr(), stream))
+        return gx
+
+
+def channel_pool_reference_ops(x: torch.Tensor) -> torch.Tensor:
+    """The reference's op sequence (attentions.py:44-47): std, lower median, mode over dim 1."""
+    stats = (x.std(dim=1, keepdim=True),
+             x.median(dim=1, keepdim=True).values,
+             x.mode(dim=1, keepdim=True).values)
+    return torch.cat(stats, dim=1)
+
+
+def native_channel_pool_applies(x: torch.Tensor) -> bool:
+    """GPU tensors of fp32/bf16/fp16 with at most 128 (fp32) / 256 channels take the HIP kernel."""
+    if not x.is_cuda or x.dim() != 4 or x.dtype not in _CHANSTAT_DTYPES or os.environ.get("ADMMTOR_CHANPOOL") == "torch":
+        return False
+    return x.shape[1] <= (128 if x.dtype == torch.float32 else 256)
+
+
 class ChannelPool(nn.Module):
-    """Per-pixel statistics across channels: unbiased std, lower median, mode (attentions.py:36-47)."""
+    """Per-pixel statistics across channels: unbiased std, lower median, mode (attentions.py:36-47).
+
+    On the GPU one HIP kernel computes all three with the reference's CPU tie rules (median: stable
+    rank (C-1)/2; mode: the smallest most frequent value, at the index libstdc++ std::sort leaves it
+    -- PyTorch's GPU mode leaves that unspecified) and a second one the backward.  CPU tensors (and
+    fp64 or very wide inputs, or ADMMTOR_CHANPOOL=torch for A/B runs) take the reference's op sequence.
+    """
 
     @staticmethod
     def forward(x: torch.Tensor) -> torch.Tensor:
-        stats = (x.std(dim=1, keepdim=True),
-                 x.median(dim=1, keepdim=True).values,
-                 x.mode(dim=1, keepdim=True).values)
-        return torch.cat(stats, dim=1)
+        if native_channel_pool_applies(x):
+            return _ChannelPoolFn.apply(x.contiguous())
+        return channel_pool_reference_ops(x)
 
 
 class SpatialGate(nn.Module):

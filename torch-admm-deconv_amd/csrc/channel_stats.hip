@@ -1,0 +1,586 @@
+// channel_stats.hip -- per-pixel channel statistics (std, median, mode) in one pass, and their
+// backward: the C ABI of include/admm_chanstat.h.  Replaces the reference's ChannelPool
+// (/root/reference/src/admmtor/elayers/attentions.py:36-47), which PyTorch runs as three
+// sort/select reductions over the channel dim of an NCHW tensor.
+//
+// Layout: x [B][C][HW].  A workgroup stages a tile of 64 consecutive pixels x C channels in LDS
+// (each load a contiguous 64-pixel row segment), then each of its 4 waves works on one pixel at a
+// time with the C values spread over its 64 lanes, so every step is wave-uniform (no per-lane
+// divergence in the data-dependent sort).  The values are "sorted" with the exact algorithm the
+// reference's CPU torch.mode uses (libstdc++ std::sort on (value, index) pairs compared by value:
+// introsort, median-of-three pivot, unguarded partition, heapsort at the depth limit, final
+// insertion sort) -- that algorithm is not stable, and the order it leaves equal values in is
+// what decides the index torch.mode returns (and so where its gradient goes).  The median's index
+// follows torch.median's rule instead (the stable rank (C-1)/2: ties broken by channel index).
+// HBM traffic is the compulsory C reads + 3 writes (+2 index writes) per pixel.
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+
+#include "admm_chanstat.h"
+#include "admm_tv.h"
+
+namespace {
+
+// ---------------------------------------------------------------- element types
+struct BF16T {
+    using store = uint16_t;
+    using key = uint32_t;
+    static constexpr int bits = 16;
+    __device__ static bool isnan(uint32_t u) { return (u & 0x7F80u) == 0x7F80u && (u & 0x7Fu); }
+    __device__ static float to_f(uint32_t u) { return __uint_as_float(u << 16); }
+    __device__ static uint16_t from_f(float f) {  // round to nearest even (PyTorch's float -> bf16)
+        uint32_t u = __float_as_uint(f);
+        if ((u & 0x7FFFFFFFu) > 0x7F800000u) return 0x7FC0;
+        u += 0x7FFFu + ((u >> 16) & 1u);
+        return (uint16_t)(u >> 16);
+    }
+};
+struct F16T {
+    using store = uint16_t;
+    using key = uint32_t;
+    static constexpr int bits = 16;
+    __device__ static bool isnan(uint32_t u) { return (u & 0x7C00u) == 0x7C00u && (u & 0x3FFu); }
+    __device__ static float to_f(uint32_t u) { return __half2float(__ushort_as_half((unsigned short)u)); }
+    __device__ static uint16_t from_f(float f) { return __half_as_ushort(__float2half_rn(f)); }
+};
+struct F32T {
+    using store = uint32_t;
+    using key = uint64_t;
+    static constexpr int bits = 32;
+    __device__ static bool isnan(uint32_t u) { return (u & 0x7FFFFFFFu) > 0x7F800000u; }
+    __device__ static float to_f(uint32_t u) { return __uint_as_float(u); }
+    __device__ static uint32_t from_f(float f) { return __float_as_uint(f); }
+};
+
+// order-preserving unsigned image of the value bits: -0 folds onto +0 (they compare equal, as the
+// reference's `<` on floats), every NaN onto the all-ones image
+template <class T> __device__ __forceinline__ uint32_t ord(uint32_t u) {
+    constexpr uint32_t sign = 1u << (T::bits - 1);
+    constexpr uint32_t all = T::bits == 32 ? 0xFFFFFFFFu : ((1u << T::bits) - 1u);
+    if (T::isnan(u)) return all;
+    if ((u & ~sign) == 0) u = 0;
+    return (u & sign) ? (~u & all) : (u | sign);
+}
+
+// ------------------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ int mbcnt(uint64_t m) {  // set bits of m below this lane
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+// LDS written by some lanes of this wave and read by others: order the accesses within the wave
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The wave's array of C elements lives in registers: position p = e * 64 + lane, e < E.
+// Reads and writes at a wave-uniform position.
+template <int E> __device__ __forceinline__ uint32_t rd(const uint32_t (&a)[E], int p) {
+    const int e = p >> 6;
+    uint32_t r = a[0];
+#pragma unroll
+    for (int k = 1; k < E; ++k)
+        if (e == k) r = a[k];
+    return (uint32_t)__builtin_amdgcn_readlane((int)r, p & 63);
+}
+template <class K, int E> __device__ __forceinline__ K rd_key(const K (&a)[E], int p) {
+    const int e = p >> 6;
+    K r = a[0];
+#pragma unroll
+    for (int k = 1; k < E; ++k)
+        if (e == k) r = a[k];
+    if constexpr (sizeof(K) == 8) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)r, p & 63);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(r >> 32), p & 63);
+        return ((K)hi << 32) | lo;
+    } else {
+        return (K)__builtin_amdgcn_readlane((int)r, p & 63);
+    }
+}
+template <int E>
+__device__ __forceinline__ void wr(uint32_t (&v)[E], uint32_t (&c)[E], int p, uint32_t vv, uint32_t cc, int lane) {
+    const int e = p >> 6;
+    if (lane == (p & 63)) {
+#pragma unroll
+        for (int k = 0; k < E; ++k)
+            if (e == k) {
+                v[k] = vv;
+                c[k] = cc;
+            }
+    }
+}
+
+// ------------------------------------------------ libstdc++ std::sort, restated (bits/stl_algo.h,
+// bits/stl_heap.h) for the comparator `a.value < b.value`.
+//
+// __unguarded_partition (Hoare) on [f+1, l) with the pivot at f, done by the whole wave at once:
+// the left scan stops at the positions holding a value >= pivot (L_1 < L_2 < ...), the right scan
+// at those holding a value <= pivot (R_1 > R_2 > ...), both judged on the values before any swap
+// (a scan never revisits a swapped position before the pointers cross), and the k-th stops swap
+// while L_k < R_k.  With S such swaps the returned cut is min(L_{S+1}, R_S) (R_0 = l).  Each lane
+// ranks its elements among the stops with ballots, the swapped pairs trade places through LDS.
+template <int E>
+__device__ int partition_wave(uint32_t (&val)[E], uint32_t (&chan)[E], int f, int l, int lane, uint64_t* sL,
+                              uint64_t* sR) {
+    const int mid = f + (l - f) / 2;
+    const uint32_t va = rd(val, f + 1), vb = rd(val, mid), vc = rd(val, l - 1);
+    int sel;  // __move_median_to_first(f, f + 1, mid, l - 1)
+    if (va < vb) sel = vb < vc ? mid : (va < vc ? l - 1 : f + 1);
+    else sel = va < vc ? f + 1 : (vb < vc ? l - 1 : mid);
+    const uint32_t v0 = rd(val, f), c0 = rd(chan, f), pv = rd(val, sel), c1 = rd(chan, sel);
+    wr(val, chan, f, pv, c1, lane);
+    wr(val, chan, sel, v0, c0, lane);
+
+    bool ge[E], le[E];
+    uint64_t gm[E], lm[E];
+    int totle = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int p = e * 64 + lane;
+        const bool in = p > f && p < l;
+        ge[e] = in && val[e] >= pv;
+        le[e] = in && val[e] <= pv;
+        gm[e] = __ballot(ge[e]);
+        lm[e] = __ballot(le[e]);
+        totle += __popcll(lm[e]);
+    }
+    int lrank[E], rrank[E];
+    bool swl[E];
+    int S = 0;
+    {
+        int gb = 0, lb = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            lrank[e] = gb + mbcnt(gm[e]);                              // # left stops before p
+            rrank[e] = totle - (lb + mbcnt(lm[e]) + (le[e] ? 1 : 0));  // # right stops after p
+            swl[e] = ge[e] && lrank[e] < rrank[e];
+            gb += __popcll(gm[e]);
+            lb += __popcll(lm[e]);
+            S += __popcll(__ballot(swl[e]));
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint64_t me = ((uint64_t)val[e] << 32) | chan[e];
+        if (swl[e]) sL[lrank[e]] = me;
+        else if (le[e] && rrank[e] < S) sR[rrank[e]] = me;
+    }
+    wave_sync();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        uint64_t in = 0;
+        bool take = false;
+        if (swl[e]) {
+            in = sR[lrank[e]];
+            take = true;
+        } else if (le[e] && rrank[e] < S) {
+            in = sL[rrank[e]];
+            take = true;
+        }
+        if (take) {
+            val[e] = (uint32_t)(in >> 32);
+            chan[e] = (uint32_t)in;
+        }
+    }
+    int lp = 1 << 30, rp = l;
+#pragma unroll
+    for (int e = E - 1; e >= 0; --e) {
+        const uint64_t m = __ballot(ge[e] && lrank[e] == S);
+        if (m) lp = e * 64 + __builtin_ctzll(m);
+        if (S > 0) {
+            const uint64_t r = __ballot(le[e] && rrank[e] == S - 1);
+            if (r) rp = e * 64 + __builtin_ctzll(r);
+        }
+    }
+    return min(lp, rp);
+}
+
+// heapsort fallback at the depth limit (std::__partial_sort(f, l, l)), run by one lane on the
+// wave's keys in LDS; reached only by adversarial orders
+template <class K> __device__ void adjust_heap(K* A, int f, int hole, int len, K v) {
+    constexpr int IB = sizeof(K) == 8 ? 32 : 16;
+    const int top = hole;
+    int sc = hole;
+    while (sc < (len - 1) / 2) {
+        sc = 2 * (sc + 1);
+        if ((A[f + sc] >> IB) < (A[f + sc - 1] >> IB)) --sc;
+        A[f + hole] = A[f + sc];
+        hole = sc;
+    }
+    if ((len & 1) == 0 && sc == (len - 2) / 2) {
+        sc = 2 * (sc + 1);
+        A[f + hole] = A[f + sc - 1];
+        hole = sc - 1;
+    }
+    int parent = (hole - 1) / 2;  // __push_heap
+    while (hole > top && (A[f + parent] >> IB) < (v >> IB)) {
+        A[f + hole] = A[f + parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    A[f + hole] = v;
+}
+
+template <class K> __device__ void heap_sort(K* A, int f, int l) {
+    const int len = l - f;
+    if (len >= 2) {
+        for (int parent = (len - 2) / 2;; --parent) {
+            adjust_heap(A, f, parent, len, A[f + parent]);
+            if (parent == 0) break;
+        }
+    }
+    for (int last = l; last - f > 1;) {
+        --last;
+        const K v = A[last];
+        A[last] = A[f];
+        adjust_heap(A, f, 0, last - f, v);
+    }
+}
+
+constexpr int WSCRATCH = 2048;  // per wave: 2 x 128 u64 swap slots (aliased by the heap keys)
+
+template <class T> constexpr int tile_row() { return sizeof(typename T::store) == 2 ? 66 : 65; }  // odd words: no bank conflicts
+
+// bitonic sort of the wave's E*64 keys (position p = e*64 + lane), ascending; every stride and
+// direction is a compile-time constant after unrolling
+template <class K, int E> __device__ __forceinline__ void wave_bitonic(K (&k)[E], int lane) {
+    constexpr int N = E * 64;
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {
+                const int es = stride >> 6;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    if ((e & es) == 0) {
+                        const bool asc = ((e * 64) & size) == 0;
+                        const K a = k[e], b = k[e | es];
+                        const K lo = a < b ? a : b, hi = a < b ? b : a;
+                        k[e] = asc ? lo : hi;
+                        k[e | es] = asc ? hi : lo;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const K o = __shfl_xor(k[e], stride);
+                    const bool asc = ((e * 64 + lane) & size) == 0;
+                    const bool lower = (lane & stride) == 0;
+                    const K mn = k[e] < o ? k[e] : o, mx = k[e] < o ? o : k[e];
+                    k[e] = asc == lower ? mn : mx;
+                }
+            }
+        }
+    }
+}
+
+// One workgroup = 4 waves and a tile of 64 consecutive pixels.  The tile [C][64] is staged in LDS
+// with coalesced row loads.  The std of each pixel is one lane's loop over its column; everything
+// else is done by one wave per pixel, its 64 lanes holding the C values (E per lane):
+//  * a wave-wide bitonic sort of (value, channel) keys gives the median (stable rank, as
+//    torch.median) and the runs of equal values, so the mode value (first longest run);
+//  * which channel torch.mode reports for it is decided by libstdc++'s introsort: the last of the
+//    mode-valued elements after the partitions (the final insertion sort is stable).  Partitioned
+//    ranges are independent and keep their order, so only the rightmost range still holding a
+//    mode-valued element matters, and only while it holds two or more: the kernel follows that one
+//    range (a few partitions per pixel instead of the whole introsort).
+template <class T, int E>
+__global__ void __launch_bounds__(256) k_chanpool(const typename T::store* __restrict__ x,
+                                                  typename T::store* __restrict__ out, int16_t* __restrict__ idx,
+                                                  int C, long long HW, long long npix, int depth_limit) {
+    using S = typename T::store;
+    using K = typename T::key;  // (value image << 8 | channel): 24 bits for 16-bit types, 40 for fp32
+    constexpr int ROW = tile_row<T>();
+    constexpr int IB = sizeof(K) == 8 ? 32 : 16;  // heap keys (value << IB | channel)
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    unsigned char* wbase = smem + wid * WSCRATCH;
+    uint64_t* sL = reinterpret_cast<uint64_t*>(wbase);              // [128]
+    uint64_t* sR = sL + 128;                                         // [128]
+    K* hk = reinterpret_cast<K*>(wbase);                             // [256] heap keys (aliases sL, sR)
+    float* res_sd = reinterpret_cast<float*>(smem + 4 * WSCRATCH);  // [64]
+    int16_t* res_mi = reinterpret_cast<int16_t*>(res_sd + 64);      // [64]
+    int16_t* res_oi = res_mi + 64;                                  // [64]
+    S* tile = reinterpret_cast<S*>(smem + 4 * WSCRATCH + 512);      // [C][ROW]
+
+    const long long P0 = (long long)blockIdx.x * 64;
+    const int npx = (int)min(64LL, npix - P0);
+    {
+        const long long gp = P0 + lane;
+        if (lane < npx) {
+            const long long b = gp / HW, hw = gp - b * HW;
+            const S* xp = x + (size_t)b * C * HW + hw;
+            for (int c = wid; c < C; c += 4) tile[c * ROW + lane] = xp[(size_t)c * HW];
+        }
+    }
+    __syncthreads();
+
+    // std: lane L of wave w owns pixel w + 4L; two-pass in fp64, channel order
+    if (lane < 16 && wid + 4 * lane < npx) {
+        const int px = wid + 4 * lane;
+        double s = 0.0;
+        for (int c = 0; c < C; ++c) s += (double)T::to_f((uint32_t)tile[c * ROW + px]);
+        const double mean = s / (double)C;
+        double m2 = 0.0;
+        for (int c = 0; c < C; ++c) {
+            const double d = (double)T::to_f((uint32_t)tile[c * ROW + px]) - mean;
+            m2 += d * d;
+        }
+        res_sd[px] = (float)sqrt(m2 / (double)(C - 1));  // C == 1: NaN, as the reference
+    }
+
+    const int mpos = (C - 1) >> 1;
+    for (int px = wid; px < npx; px += 4) {
+        uint32_t val[E], chan[E];
+        K key[E];
+        bool valid[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int p = e * 64 + lane;
+            valid[e] = p < C;
+            val[e] = valid[e] ? ord<T>((uint32_t)tile[p * ROW + px]) : 0xFFFFFFFFu;
+            chan[e] = (uint32_t)p;
+            key[e] = valid[e] ? (((K)val[e] << 8) | (K)p) : ~(K)0;
+        }
+        wave_bitonic(key, lane);
+
+        // median: sorted position mpos of the (value, channel) order
+        const int mi = (int)(rd_key(key, mpos) & 0xFF);
+
+        // runs of equal values in the sorted keys: starts, lengths, the first longest run
+        uint32_t sv[E];
+        bool start[E];
+        uint64_t sm[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            sv[e] = (uint32_t)(key[e] >> 8);
+            const uint32_t carry = e > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)sv[e > 0 ? e - 1 : 0], 63) : 0u;
+            uint32_t prev = (uint32_t)__shfl_up((int)sv[e], 1);
+            if (lane == 0) prev = e > 0 ? carry : ~sv[e];
+            const int p = e * 64 + lane;
+            start[e] = p < C && sv[e] != prev;
+            sm[e] = __ballot(start[e]);
+        }
+        uint32_t len[E], lmax = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int p = e * 64 + lane;
+            int next = C;
+#pragma unroll
+            for (int e2 = E - 1; e2 > e; --e2)
+                if (sm[e2]) next = e2 * 64 + __builtin_ctzll(sm[e2]);
+            const uint64_t above = lane < 63 ? sm[e] >> (lane + 1) : 0ull;
+            if (above) next = p + 1 + __builtin_ctzll(above);
+            len[e] = start[e] ? (uint32_t)(next - p) : 0u;
+            lmax = max(lmax, len[e]);
+        }
+        lmax = wave_max(lmax);
+        int ms = -1;  // position of the mode run's first key
+#pragma unroll
+        for (int e = E - 1; e >= 0; --e) {
+            const uint64_t m = __ballot(len[e] == lmax && start[e]);
+            if (m) ms = e * 64 + __builtin_ctzll(m);
+        }
+        const uint32_t mvl = (uint32_t)(rd_key(key, ms) >> 8);
+
+        int oi;
+        if (lmax == 1 || C <= 16) {
+            // a unique value, or no partition at all (only the stable insertion sort): the run's
+            // last key in (value, channel) order
+            oi = (int)(rd_key(key, ms + (int)lmax - 1) & 0xFF);
+        } else {
+            const int lg = 31 - __builtin_clz((unsigned)C);
+            int f = 0, l = C, depth = depth_limit < 0 ? 2 * lg : depth_limit;
+            for (;;) {
+                // mode-valued elements in [f, l): how many, and the last one
+                int cntm = 0, lastp = -1;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int p = e * 64 + lane;
+                    const uint64_t m = __ballot(p >= f && p < l && val[e] == mvl);
+                    cntm += __popcll(m);
+                    if (m) lastp = e * 64 + 63 - __builtin_clzll(m);
+                }
+                if (cntm == 1 || l - f <= 16) {
+                    oi = (int)rd(chan, lastp);
+                    break;
+                }
+                if (depth == 0) {
+                    wave_sync();
+#pragma unroll
+                    for (int e = 0; e < E; ++e)
+                        if (valid[e]) hk[e * 64 + lane] = ((K)val[e] << IB) | (K)chan[e];
+                    wave_sync();
+                    if (lane == 0) heap_sort(hk, f, l);
+                    wave_sync();
+                    int best = -1;
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int p = e * 64 + lane;
+                        if (p >= f && p < l) {
+                            const K k = hk[p];
+                            if ((uint32_t)(k >> IB) == mvl) best = p;
+                        }
+                    }
+                    const int bp = (int)wave_max((uint32_t)(best + 1)) - 1;
+                    oi = (int)(hk[bp] & (K)0xFFFF);
+                    break;
+                }
+                --depth;
+                const int cut = partition_wave(val, chan, f, l, lane, sL, sR);
+                bool right = false;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int p = e * 64 + lane;
+                    right |= __ballot(p >= cut && p < l && val[e] == mvl) != 0;
+                }
+                if (right) f = cut;
+                else l = cut;
+            }
+        }
+        if (lane == 0) {
+            res_mi[px] = (int16_t)mi;
+            res_oi[px] = (int16_t)oi;
+        }
+    }
+    __syncthreads();
+    {
+        const int px = lane, k = wid;
+        if (px < npx) {
+            const long long gp = P0 + px;
+            const long long b = gp / HW, hw = gp - b * HW;
+            if (k < 3) {
+                // the selected elements themselves (keeps -0.0 and NaN payloads)
+                const S v = k == 0 ? (S)T::from_f(res_sd[px]) : tile[(k == 1 ? res_mi[px] : res_oi[px]) * ROW + px];
+                out[((size_t)b * 3 + k) * HW + hw] = v;
+            } else if (idx) {
+                idx[(size_t)b * 2 * HW + hw] = res_mi[px];
+                idx[((size_t)b * 2 + 1) * HW + hw] = res_oi[px];
+            }
+        }
+    }
+}
+
+// backward: gx_c = g_std (x_c - mean) / ((C-1) std) + [c == mi] g_med + [c == oi] g_mode, in fp32
+// with the std the forward returned (the reference's std_backward uses its result)
+template <class T>
+__global__ void __launch_bounds__(256) k_chanpool_bwd(const typename T::store* __restrict__ x,
+                                                      const typename T::store* __restrict__ out,
+                                                      const int16_t* __restrict__ idx,
+                                                      const typename T::store* __restrict__ gout,
+                                                      typename T::store* __restrict__ gx, int C, long long HW,
+                                                      long long npix) {
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (p >= npix) return;
+    const long long b = p / HW, hw = p - b * HW;
+    const typename T::store* xp = x + (size_t)b * C * HW + hw;
+    typename T::store* gp = gx + (size_t)b * C * HW + hw;
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += T::to_f(xp[(size_t)c * HW]);
+    const float mean = s / (float)C;
+    const size_t o3 = (size_t)b * 3 * HW + hw, o2 = (size_t)b * 2 * HW + hw;
+    const float sd = T::to_f(out[o3]);
+    const float gs = T::to_f(gout[o3]), gm = T::to_f(gout[o3 + HW]), go = T::to_f(gout[o3 + 2 * HW]);
+    const int mi = idx[o2], oi = idx[o2 + HW];
+    const float scale = sd == 0.f ? 0.f : gs / ((float)(C - 1) * sd);  // std_backward's masked_fill_(std == 0, 0)
+    for (int c = 0; c < C; ++c) {
+        float g = scale * (T::to_f(xp[(size_t)c * HW]) - mean);
+        if (c == mi) g += gm;
+        if (c == oi) g += go;
+        gp[(size_t)c * HW] = T::from_f(g);
+    }
+}
+
+size_t lds_bytes(int dtype, int64_t C) {
+    const size_t row = dtype == ADMM_CHANSTAT_F32 ? 65 * 4 : 66 * 2;
+    return 4 * WSCRATCH + 512 + (size_t)C * row;
+}
+
+template <class T, int E>
+int launch_e(const void* x, int64_t B, int64_t C, int64_t HW, void* out, int16_t* idx, size_t lds, int depth,
+             hipStream_t s) {
+    const long long npix = (long long)B * HW;
+    if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chanpool<T, E>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return ADMM_TV_EHIP;
+    hipLaunchKernelGGL((k_chanpool<T, E>), dim3((unsigned)((npix + 63) / 64)), dim3(256), lds, s,
+                       static_cast<const typename T::store*>(x), static_cast<typename T::store*>(out), idx, (int)C,
+                       (long long)HW, npix, depth);
+    return hipGetLastError() == hipSuccess ? 0 : ADMM_TV_EHIP;
+}
+
+template <class T>
+int launch(const void* x, int64_t B, int64_t C, int64_t HW, void* out, int16_t* idx, size_t lds, int depth,
+           hipStream_t s) {
+    if (C <= 64) return launch_e<T, 1>(x, B, C, HW, out, idx, lds, depth, s);
+    if (C <= 128) return launch_e<T, 2>(x, B, C, HW, out, idx, lds, depth, s);
+    if constexpr (sizeof(typename T::store) == 2) return launch_e<T, 4>(x, B, C, HW, out, idx, lds, depth, s);
+    return ADMM_TV_EUNSUPPORTED;
+}
+
+template <class T>
+int launch_bwd(const void* x, const void* out, const int16_t* idx, const void* gout, void* gx, int64_t B, int64_t C,
+               int64_t HW, hipStream_t s) {
+    const long long npix = (long long)B * HW;
+    hipLaunchKernelGGL((k_chanpool_bwd<T>), dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const typename T::store*>(x), static_cast<const typename T::store*>(out), idx,
+                       static_cast<const typename T::store*>(gout), static_cast<typename T::store*>(gx), (int)C,
+                       (long long)HW, npix);
+    return hipGetLastError() == hipSuccess ? 0 : ADMM_TV_EHIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+int admm_chanstat_max_channels(int dtype) {
+    return dtype == ADMM_CHANSTAT_F32 ? 128 : (dtype == ADMM_CHANSTAT_BF16 || dtype == ADMM_CHANSTAT_F16) ? 256 : 0;
+}
+
+int admm_chanstat_pool_depth(int dtype, const void* x, int64_t B, int64_t C, int64_t HW, void* out, int16_t* idx,
+                             int depth_limit, void* stream) {
+    if (depth_limit > 16) return ADMM_TV_EINVAL;
+    if (!x || !out || B < 0 || C < 1 || HW < 0) return ADMM_TV_EINVAL;
+    if (C > admm_chanstat_max_channels(dtype)) return ADMM_TV_EUNSUPPORTED;
+    if (B == 0 || HW == 0) return 0;
+    if (B * HW > 0x7FFFFFFFLL * 64) return ADMM_TV_EUNSUPPORTED;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t lds = lds_bytes(dtype, C);
+    switch (dtype) {
+        case ADMM_CHANSTAT_BF16: return launch<BF16T>(x, B, C, HW, out, idx, lds, depth_limit, s);
+        case ADMM_CHANSTAT_F16: return launch<F16T>(x, B, C, HW, out, idx, lds, depth_limit, s);
+        case ADMM_CHANSTAT_F32: return launch<F32T>(x, B, C, HW, out, idx, lds, depth_limit, s);
+        default: return ADMM_TV_EINVAL;
+    }
+}
+
+int admm_chanstat_pool(int dtype, const void* x, int64_t B, int64_t C, int64_t HW, void* out, int16_t* idx,
+                       void* stream) {
+    return admm_chanstat_pool_depth(dtype, x, B, C, HW, out, idx, -1, stream);
+}
+
+int admm_chanstat_pool_backward(int dtype, const void* x, const void* out, const int16_t* idx, const void* gout,
+                                int64_t B, int64_t C, int64_t HW, void* gx, void* stream) {
+    if (!x || !out || !idx || !gout || !gx || B < 0 || C < 1 || HW < 0) return ADMM_TV_EINVAL;
+    if (C > admm_chanstat_max_channels(dtype)) return ADMM_TV_EUNSUPPORTED;
+    if (B == 0 || HW == 0) return 0;
+    if (B * HW > 0x7FFFFFFFLL * 256) return ADMM_TV_EUNSUPPORTED;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case ADMM_CHANSTAT_BF16: return launch_bwd<BF16T>(x, out, idx, gout, gx, B, C, HW, s);
+        case ADMM_CHANSTAT_F16: return launch_bwd<F16T>(x, out, idx, gout, gx, B, C, HW, s);
+        case ADMM_CHANSTAT_F32: return launch_bwd<F32T>(x, out, idx, gout, gx, B, C, HW, s);
+        default: return ADMM_TV_EINVAL;
+    }
+}
+
+}  // extern "C"
