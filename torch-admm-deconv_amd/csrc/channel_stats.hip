@@ -68,11 +68,40 @@ template <class T> __device__ __forceinline__ uint32_t ord(uint32_t u) {
 __device__ __forceinline__ int mbcnt(uint64_t m) {  // set bits of m below this lane
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
+// lane i <-> lane i ^ M within the wave, on VALU cross-lane paths only (DPP, v_permlane*_swap):
+// no LDS round trip.  quad_perm for 1/2/3, row_half_mirror (i ^ 7), row_ror:8 (i ^ 8 in a
+// 16-lane row), row_mirror (i ^ 15), permlane16/32_swap for 16/32; the rest compose.
+template <int M> __device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lane) {
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);
+    else if constexpr (M == 7) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+    else if constexpr (M == 4) return xor_lane<7>(xor_lane<3>(v, lane), lane);
+    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+    else if constexpr (M == 15) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
+    else if constexpr (M == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else if constexpr (M == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    } else if constexpr (M == 31) return xor_lane<15>(xor_lane<16>(v, lane), lane);
+    else if constexpr (M == 63) return xor_lane<31>(xor_lane<32>(v, lane), lane);
+    else static_assert(M == 0, "unsupported lane mask");
 }
+template <int M> __device__ __forceinline__ uint64_t xor_lane(uint64_t v, int lane) {
+    return ((uint64_t)xor_lane<M>((uint32_t)(v >> 32), lane) << 32) | xor_lane<M>((uint32_t)v, lane);
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v, int lane) {
+    v = max(v, xor_lane<1>(v, lane));
+    v = max(v, xor_lane<2>(v, lane));
+    v = max(v, xor_lane<4>(v, lane));
+    v = max(v, xor_lane<8>(v, lane));
+    v = max(v, xor_lane<16>(v, lane));
+    return max(v, xor_lane<32>(v, lane));
+}
+
 // LDS written by some lanes of this wave and read by others: order the accesses within the wave
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -249,38 +278,62 @@ constexpr int WSCRATCH = 2048;  // per wave: 2 x 128 u64 swap slots (aliased by 
 
 template <class T> constexpr int tile_row() { return sizeof(typename T::store) == 2 ? 66 : 65; }  // odd words: no bank conflicts
 
-// bitonic sort of the wave's E*64 keys (position p = e*64 + lane), ascending; every stride and
-// direction is a compile-time constant after unrolling
-template <class K, int E> __device__ __forceinline__ void wave_bitonic(K (&k)[E], int lane) {
-    constexpr int N = E * 64;
+// One compare-exchange stage of the sort over the wave's E*64 keys (position p = e*64 + lane):
+// p meets p ^ MASK, the lower position keeps the smaller key.  MASK's lane part moves through
+// xor_lane, its register part (>= 64) is a register pair within the lane.
+template <int MASK, class K, int E> __device__ __forceinline__ void cx_stage(K (&k)[E], int lane) {
+    constexpr int ML = MASK & 63, ME = MASK >> 6;
+    if constexpr (ME == 0) {
+        constexpr int HB = 1 << (31 - __builtin_clz(ML));
+        const bool low = (lane & HB) == 0;
 #pragma unroll
-    for (int size = 2; size <= N; size <<= 1) {
+        for (int e = 0; e < E; ++e) {
+            const K o = xor_lane<ML>(k[e], lane);
+            k[e] = (low == (k[e] < o)) ? k[e] : o;
+        }
+    } else {
+        constexpr int HE = 1 << (31 - __builtin_clz(ME));
 #pragma unroll
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            if (stride >= 64) {
-                const int es = stride >> 6;
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    if ((e & es) == 0) {
-                        const bool asc = ((e * 64) & size) == 0;
-                        const K a = k[e], b = k[e | es];
-                        const K lo = a < b ? a : b, hi = a < b ? b : a;
-                        k[e] = asc ? lo : hi;
-                        k[e | es] = asc ? hi : lo;
-                    }
+        for (int e = 0; e < E; ++e) {
+            if ((e & HE) == 0 && (e ^ ME) < E) {
+                const int e2 = e ^ ME;
+                K o1, o2;
+                if constexpr (ML == 0) {
+                    o1 = k[e2];
+                    o2 = k[e];
+                } else {
+                    o1 = xor_lane<ML>(k[e2], lane);
+                    o2 = xor_lane<ML>(k[e], lane);
                 }
-            } else {
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const K o = __shfl_xor(k[e], stride);
-                    const bool asc = ((e * 64 + lane) & size) == 0;
-                    const bool lower = (lane & stride) == 0;
-                    const K mn = k[e] < o ? k[e] : o, mx = k[e] < o ? o : k[e];
-                    k[e] = asc == lower ? mn : mx;
-                }
+                k[e] = k[e] < o1 ? k[e] : o1;
+                k[e2] = k[e2] < o2 ? o2 : k[e2];
             }
         }
     }
+}
+
+// merge step of size N: the mirror stage (p ^ (N-1)) then half-cleaners p ^ N/4 ... p ^ 1
+template <int N, class K, int E> __device__ __forceinline__ void merge_stages(K (&k)[E], int lane) {
+    cx_stage<N - 1>(k, lane);
+    if constexpr (N >= 256) cx_stage<64>(k, lane);
+    if constexpr (N >= 128) cx_stage<32>(k, lane);
+    if constexpr (N >= 64) cx_stage<16>(k, lane);
+    if constexpr (N >= 32) cx_stage<8>(k, lane);
+    if constexpr (N >= 16) cx_stage<4>(k, lane);
+    if constexpr (N >= 8) cx_stage<2>(k, lane);
+    if constexpr (N >= 4) cx_stage<1>(k, lane);
+}
+
+// ascending bitonic sort of the wave's E*64 keys, every exchange on VALU cross-lane paths
+template <class K, int E> __device__ __forceinline__ void wave_bitonic(K (&k)[E], int lane) {
+    merge_stages<2>(k, lane);
+    merge_stages<4>(k, lane);
+    merge_stages<8>(k, lane);
+    merge_stages<16>(k, lane);
+    merge_stages<32>(k, lane);
+    merge_stages<64>(k, lane);
+    if constexpr (E >= 2) merge_stages<128>(k, lane);
+    if constexpr (E >= 4) merge_stages<256>(k, lane);
 }
 
 // One workgroup = 4 waves and a tile of 64 consecutive pixels.  The tile [C][64] is staged in LDS
@@ -383,7 +436,7 @@ __global__ void __launch_bounds__(256) k_chanpool(const typename T::store* __res
             len[e] = start[e] ? (uint32_t)(next - p) : 0u;
             lmax = max(lmax, len[e]);
         }
-        lmax = wave_max(lmax);
+        lmax = wave_max(lmax, lane);
         int ms = -1;  // position of the mode run's first key
 #pragma unroll
         for (int e = E - 1; e >= 0; --e) {
@@ -431,7 +484,7 @@ __global__ void __launch_bounds__(256) k_chanpool(const typename T::store* __res
                             if ((uint32_t)(k >> IB) == mvl) best = p;
                         }
                     }
-                    const int bp = (int)wave_max((uint32_t)(best + 1)) - 1;
+                    const int bp = (int)wave_max((uint32_t)(best + 1), lane) - 1;
                     oi = (int)(hk[bp] & (K)0xFFFF);
                     break;
                 }
