@@ -9,6 +9,13 @@ __global__ void calib_copy8(const float2* __restrict__ a, float2* __restrict__ b
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
         b[i] = a[i];
 }
+// the same with non-temporal loads and stores (pass A's cache policy, ADMM_NT)
+typedef float v2f __attribute__((ext_vector_type(2)));
+__global__ void calib_copy8nt(const float2* __restrict__ a, float2* __restrict__ b, long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const v2f*>(a) + i),
+                                    reinterpret_cast<v2f*>(b) + i);
+}
 // 16-byte per lane streaming (the guide's calibrated case)
 __global__ void calib_copy16(const float4* __restrict__ a, float4* __restrict__ b, long long n) {
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
@@ -32,6 +39,8 @@ extern "C" int calib_run(int kind, const void* a, void* b, long long bytes, int 
         hipLaunchKernelGGL(calib_copy8, dim3(8192), dim3(256), 0, s, (const float2*)a, (float2*)b, bytes / 8);
     } else if (kind == 1) {
         hipLaunchKernelGGL(calib_copy16, dim3(8192), dim3(256), 0, s, (const float4*)a, (float4*)b, bytes / 16);
+    } else if (kind == 3) {
+        hipLaunchKernelGGL(calib_copy8nt, dim3(8192), dim3(256), 0, s, (const float2*)a, (float2*)b, bytes / 8);
     } else {
         const long long planes = bytes / ((long long)H * N * 8);
         const int cbs = N / 8;

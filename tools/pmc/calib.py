@@ -7,7 +7,7 @@ n = 1 << 30
 a = torch.rand(n // 4, device="cuda")
 b = torch.empty_like(a)
 s = torch.cuda.current_stream().cuda_stream
-for kind in (0, 1, 2):
+for kind in (0, 1, 2, 3):
     for _ in range(3):
         assert lib.calib_run(kind, a.data_ptr(), b.data_ptr(), n, 1024, 512, s) == 0
 torch.cuda.synchronize()

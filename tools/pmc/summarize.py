@@ -25,9 +25,10 @@ def main(src, dst):
     gib_kb = float(1 << 20)
     cal = {}
     for name in f_cal:
-        for tag in ("calib_copy8", "calib_copy16", "calib_cols"):
+        for tag in ("calib_copy8nt", "calib_copy8", "calib_copy16", "calib_cols"):
             if name.startswith(tag):
                 cal[tag] = {"fetch_factor": gib_kb / f_cal[name], "write_factor": gib_kb / w_cal[name]}
+                break
     fetch, nf = load(os.path.join(src, "bench_FETCH_SIZE", "run_counter_collection.csv"))
     write, nw = load(os.path.join(src, "bench_WRITE_SIZE", "run_counter_collection.csv"))
     # C3 bench workload: 64x3x1024x1024 fp32 pixels
@@ -37,7 +38,10 @@ def main(src, dst):
         if "admm::" not in name:
             continue
         short = name.split("(")[0].replace("void admm::", "").replace("admm::", "")
-        ff = cal["calib_copy8"]["fetch_factor"]  # row kernels stream contiguous 512-B wave segments
+        # row kernels stream contiguous 512-B wave segments; pass A with non-temporal loads
+        ff = cal["calib_copy8"]["fetch_factor"]
+        if short.startswith("k_pass_a") and "calib_copy8nt" in cal:
+            ff = cal["calib_copy8nt"]["fetch_factor"]
         alg = None
         if short.startswith("k_pass_a") and short.endswith("false, false, false>"):
             alg = 28 * npx

@@ -73,6 +73,10 @@ template <int N, bool ISO, bool LASTK, bool FIRSTK>
 __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a) {
     using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
+    // streaming history / adjoint images and the spectra non-temporal, as the forward's pass A;
+    // the per-module norm and Q maps (re-read by every plane) stay cacheable
+    constexpr bool kNT = ADMM_NT_BWD != 0;
+    constexpr bool kSpecNT = kNT && ((ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
     load_tw(tw, a.twW, W);
@@ -113,14 +117,14 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
     {
         const int g = (i0 - 1 + H) & (H - 1);
 #pragma unroll
-        for (int j = 0; j < E; ++j) rprev[j] = sp[(size_t)g * N + t + L * j];
+        for (int j = 0; j < E; ++j) rprev[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + L * j]);
         RowXf<N>::c2r(rprev, buf, tw, t);
     }
     for (int rr = 0; rr <= R; ++rr) {
         const int g = (i0 + rr) & (H - 1);
         const size_t ro = (size_t)g * N;
 #pragma unroll
-        for (int j = 0; j < E; ++j) rcur[j] = sp[ro + t + L * j];
+        for (int j = 0; j < E; ++j) rcur[j] = ld_pol<kSpecNT>(&sp[ro + t + L * j]);
         RowXf<N>::c2r(rcur, buf, tw, t);
 
         // ---- y direction at row g
@@ -132,20 +136,20 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
                 const float d0 = rcur[j].x - rprev[j].x, d1 = rcur[j].y - rprev[j].y;  // Dy r^
                 cf ap = mkc(0.f, 0.f), npv = mkc(0.f, 0.f);
                 if constexpr (!FIRSTK) {
-                    ap = apy[i];
+                    ap = ld_pol<kNT>(&apy[i]);
                     if constexpr (ISO) npv = npy[i];
                 }
                 const float zp0 = FIRSTK ? 0.f : shrink_z<ISO>(ap.x, tau, npv.x);
                 const float zp1 = FIRSTK ? 0.f : shrink_z<ISO>(ap.y, tau, npv.y);
                 if (rr < R) {
                     // rho^ += Dy r^ . (w_{k-1} - Dy x_k),  w = 2z - a,  Dy x_k = a_k - u_{k-1} = a_k - a_p + z_p
-                    const cf ak = aky[i];
+                    const cf ak = ld_pol<kNT>(&aky[i]);
                     const float e0 = (2.f * zp0 - ap.x) - (ak.x - ap.x + zp0);
                     const float e1 = (2.f * zp1 - ap.y) - (ak.y - ap.y + zp1);
                     rho_acc = fmaf(d0, e0, fmaf(d1, e1, rho_acc));
                 }
                 if constexpr (!FIRSTK) {
-                    const cf ub = LASTK ? mkc(0.f, 0.f) : abyi[i];
+                    const cf ub = LASTK ? mkc(0.f, 0.f) : ld_pol<kNT>(&abyi[i]);
                     const float wb0 = rho * d0, wb1 = rho * d1;
                     const float zb0 = 2.f * wb0 - ub.x, zb1 = 2.f * wb1 - ub.y;
                     cf q = mkc(0.f, 0.f);
@@ -160,7 +164,7 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
             if constexpr (!FIRSTK) {
                 if (rr < R) {
 #pragma unroll
-                    for (int j = 0; j < E; ++j) abyo[ro + t + L * j] = abyc[j];
+                    for (int j = 0; j < E; ++j) st_pol<kNT>(&abyo[ro + t + L * j], abyc[j]);
                 }
             }
         }
@@ -170,10 +174,10 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
             for (int j = 0; j < E; ++j) {
                 cf v = rcur[j];
                 if constexpr (!LASTK) {
-                    const cf o = bb[ro + t + L * j];
+                    const cf o = ld_pol<kNT>(&bb[ro + t + L * j]);
                     v = mkc(o.x + v.x, o.y + v.y);
                 }
-                bb[ro + t + L * j] = v;
+                st_pol<kNT>(&bb[ro + t + L * j], v);
             }
         }
         // ---- finalize x^_{k-1} at row g-1: D^T a^ = (a^x[j] - a^x[j+1]) + (a^y[g-1] - a^y[g])
@@ -192,7 +196,7 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
                 }
                 RowXf<N>::r2c(r, buf, tw, t);
 #pragma unroll
-                for (int j = 0; j < E; ++j) so[rm + t + L * j] = r[j];
+                for (int j = 0; j < E; ++j) st_pol<kNT>(&so[rm + t + L * j], r[j]);
             }
         }
         // ---- x direction at row g
@@ -207,17 +211,17 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
                 const float d0 = rcur[j].x - rl, d1 = rcur[j].y - rcur[j].x;  // Dx r^
                 cf ap = mkc(0.f, 0.f), npv = mkc(0.f, 0.f);
                 if constexpr (!FIRSTK) {
-                    ap = apx[i];
+                    ap = ld_pol<kNT>(&apx[i]);
                     if constexpr (ISO) npv = npx[i];
                 }
                 const float zp0 = FIRSTK ? 0.f : shrink_z<ISO>(ap.x, tau, npv.x);
                 const float zp1 = FIRSTK ? 0.f : shrink_z<ISO>(ap.y, tau, npv.y);
-                const cf ak = akx[i];
+                const cf ak = ld_pol<kNT>(&akx[i]);
                 const float e0 = (2.f * zp0 - ap.x) - (ak.x - ap.x + zp0);
                 const float e1 = (2.f * zp1 - ap.y) - (ak.y - ap.y + zp1);
                 rho_acc = fmaf(d0, e0, fmaf(d1, e1, rho_acc));
                 if constexpr (!FIRSTK) {
-                    const cf ub = LASTK ? mkc(0.f, 0.f) : abxi[i];
+                    const cf ub = LASTK ? mkc(0.f, 0.f) : ld_pol<kNT>(&abxi[i]);
                     const float wb0 = rho * d0, wb1 = rho * d1;
                     const float zb0 = 2.f * wb0 - ub.x, zb1 = 2.f * wb1 - ub.y;
                     cf q = mkc(0.f, 0.f);
@@ -229,7 +233,7 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
             }
             if constexpr (!FIRSTK) {
 #pragma unroll
-                for (int j = 0; j < E; ++j) abxo[ro + t + L * j] = abxp[j];
+                for (int j = 0; j < E; ++j) st_pol<kNT>(&abxo[ro + t + L * j], abxp[j]);
             }
         }
 #pragma unroll

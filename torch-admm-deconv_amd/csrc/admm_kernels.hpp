@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
     const int sstep = L * N * (int)sizeof(cf);
     cf v[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) v[j] = bload_cf(rs, voff, j * sstep);
+    for (int j = 0; j < E; ++j) v[j] = bload_cf<(ADMM_NT & 8) ? 2 : 0>(rs, voff, j * sstep);
     // multipliers for this column, prefetched with the data (L2-resident tables)
     using MT = typename std::conditional<MODE == 0, float, cf>::type;
     MT m[E];
@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
     }
     fft<H, L, +1, 1, 1>(v, buf, tw, t);
 #pragma unroll
-    for (int j = 0; j < E; ++j) bstore_cf(ro, voff, j * sstep, v[j]);
+    for (int j = 0; j < E; ++j) bstore_cf<(ADMM_NT & 4) ? 2 : 0>(ro, voff, j * sstep, v[j]);
 }
 
 // Pass B (MODE 0) with two adjacent columns per thread: 16-byte loads and stores, so the 8
@@ -460,7 +460,7 @@ __device__ __forceinline__ cf prev_u(const cf* __restrict__ src, const cf* __res
     if constexpr (FIRST) {
         return mkc(0.f, 0.f);
     } else {
-        const cf v = src[idx];
+        const cf v = lda<16>(&src[idx]);
         if constexpr (HIST) {
             const cf n = ISO ? nsp[idx] : mkc(0.f, 0.f);
             return mkc(v.x - shrink_z<ISO>(v.x, tau, n.x), v.y - shrink_z<ISO>(v.y, tau, n.y));
@@ -474,6 +474,7 @@ template <int N, bool ISO, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
     using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
+    constexpr bool kSpecNT = (ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
     load_tw(tw, a.twW, W);
@@ -508,14 +509,14 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
     {
         const int g = (i0 - 1 + H) & (H - 1);
 #pragma unroll
-        for (int j = 0; j < E; ++j) xprev[j] = sp[(size_t)g * N + t + L * j];
+        for (int j = 0; j < E; ++j) xprev[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + L * j]);
         RowXf<N>::c2r(xprev, buf, tw, t);
     }
     for (int rr = 0; rr <= R; ++rr) {
         const int g = (i0 + rr) & (H - 1);
         const size_t ro = (size_t)g * N;  // row offset in cf units (spectrum and pixel pairs alike)
 #pragma unroll
-        for (int j = 0; j < E; ++j) xcur[j] = sp[ro + t + L * j];
+        for (int j = 0; j < E; ++j) xcur[j] = ld_pol<kSpecNT>(&sp[ro + t + L * j]);
         RowXf<N>::c2r(xcur, buf, tw, t);
 
         // ---- y direction: a_y = x[g] - x[g-1] + u_y; z_y, u_y, w_y of row g
@@ -539,7 +540,7 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
             }
             if (rr < R) {
 #pragma unroll
-                for (int j = 0; j < E; ++j) uyo[ro + t + L * j] = uy[j];
+                for (int j = 0; j < E; ++j) sta(&uyo[ro + t + L * j], uy[j]);
             }
         }
 
@@ -553,14 +554,14 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
 #pragma unroll
             for (int j = 0; j < E; ++j) {
                 const float wr = (t == L - 1) ? sh[(j + 1) & (E - 1)].x : sh[j].x;  // w_x at pixel q1+1
-                const cf bb = bimg[rm + t + L * j];
+                const cf bb = lda<16>(&bimg[rm + t + L * j]);
                 const float v0 = (wxp[j].x - wxp[j].y) + (wyp[j].x - wyc[j].x);
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
                 r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
             }
             RowXf<N>::r2c(r, buf, tw, t);
 #pragma unroll
-            for (int j = 0; j < E; ++j) so[rm + t + L * j] = r[j];
+            for (int j = 0; j < E; ++j) sta(&so[rm + t + L * j], r[j]);
         }
 
         // ---- x direction: a_x = x[g][j] - x[g][j-1] + u_x; z_x, u_x, w_x of row g
@@ -584,7 +585,7 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
                 wxp[j] = mkc(z0 - n0, z1 - n1);
             }
 #pragma unroll
-            for (int j = 0; j < E; ++j) uxo[ro + t + L * j] = ux[j];
+            for (int j = 0; j < E; ++j) sta(&uxo[ro + t + L * j], ux[j]);
         }
 #pragma unroll
         for (int j = 0; j < E; ++j) {

@@ -98,12 +98,40 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
-__device__ __forceinline__ cf bload_cf(rsrc_t r, int voff, int soff) {
-    return __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+// AUX: cache policy bits (2 = nt, streaming)
+template <int AUX = 0> __device__ __forceinline__ cf bload_cf(rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX));
 }
-__device__ __forceinline__ void bstore_cf(rsrc_t r, int voff, int soff, cf v) {
+template <int AUX = 0> __device__ __forceinline__ void bstore_cf(rsrc_t r, int voff, int soff, cf v) {
     typedef decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)) V2;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, voff, soff, AUX);
+}
+
+// Streaming-data cache policy of pass A (-DADMM_NT=mask overrides for A/B runs): bit 0 stores nt,
+// bit 1 spectrum loads nt, bit 5 spectrum loads nt only for W >= 1024, bit 4 u / b loads nt; bit 2
+// pass B stores nt, bit 3 pass B loads nt.  Default 0x31, measured (tools/ab_variants.sh,
+// DESIGN.md §4): C3 666 -> 706 it/s, C2 4702 -> 5213 it/s; nt in pass B is slower (its paired
+// column blocks share lines through L2).
+#ifndef ADMM_NT
+#define ADMM_NT 0x31
+#endif
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+template <bool NT> __device__ __forceinline__ cf ld_pol(const cf* p) {
+    if constexpr (NT) return __builtin_bit_cast(cf, __builtin_nontemporal_load(reinterpret_cast<const v2f_t*>(p)));
+    else return *p;
+}
+template <int BIT = 2> __device__ __forceinline__ cf lda(const cf* p) { return ld_pol<(ADMM_NT & BIT) != 0>(p); }
+template <bool NT> __device__ __forceinline__ void st_pol(cf* p, cf v) {
+    if constexpr (NT) __builtin_nontemporal_store(__builtin_bit_cast(v2f_t, v), reinterpret_cast<v2f_t*>(p));
+    else *p = v;
+}
+// the training backward's reverse row pass (-DADMM_NT_BWD=0 for A/B runs)
+#ifndef ADMM_NT_BWD
+#define ADMM_NT_BWD 1
+#endif
+__device__ __forceinline__ void sta(cf* p, cf v) {
+    if constexpr ((ADMM_NT & 1) != 0) __builtin_nontemporal_store(__builtin_bit_cast(v2f_t, v), reinterpret_cast<v2f_t*>(p));
+    else *p = v;
 }
 __device__ __forceinline__ float bload_f(rsrc_t r, int voff, int soff) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
