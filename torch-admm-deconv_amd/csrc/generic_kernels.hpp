@@ -93,44 +93,91 @@ __device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restr
     }
 }
 
-// any radix R: one output element per item, O(R) work.  The twiddle exponent q (m + k NS) mod
-// (NS R) is stepped incrementally (no integer modulo in the inner loop).
+// any (odd prime) radix R, in two steps:
+//  1. the stage twiddles W_{NS R}^{m q} are applied to the inputs in place (src is this stage's
+//     scratch), so what remains per butterfly is a plain R-point DFT;
+//  2. outputs k and R - k take conjugate twiddles W_R^{+-qk}: an item computes GP such output
+//     pairs of one butterfly (group 0 also output 0), reading each input once and each table
+//     twiddle once for both outputs of a pair -- (1 + GP) LDS reads per input for 2 GP outputs
+//     instead of 2 per input per output, and the two complex products share their four real
+//     multiplies.
+#ifndef ADMM_GP
+#define ADMM_GP 2
+#endif
+#ifndef ADMM_GUNROLL
+#define ADMM_GUNROLL 8
+#endif
+constexpr int GP = ADMM_GP;
+
 template <int DIR>
-__device__ __forceinline__ void gstage_any(const cf* __restrict__ src, cf* __restrict__ dst, int n, int NS, int R,
+__device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict__ dst, int n, int NS, int R,
                                            int lines, const cf* __restrict__ tw) {
     const int nb = n / R;
     const int span = NS * R;
     const int tstride = n / span;
-    for (int item = threadIdx.x; item < n * lines; item += blockDim.x) {
-        const int c = item % lines, o = item / lines;  // o = vt-major output slot (vt, k)
-        const int vt = o % nb, k = o / nb;
-        const int m = vt % NS;
-        const int e = m + k * NS;  // exponent step: W_{NS R}^{q e}
-        const cf* col = src + vt * lines + c;
-        const int qstep = nb * lines;
-        // two interleaved accumulators (even / odd q) halve the dependent chain
-        cf acc0 = col[0], acc1 = mkc(0.f, 0.f);
-        int idx = e >= span ? e - span : e;  // q = 1
-        const int e2 = (2 * e) % span;
-        int idx2 = idx + e;
-        if (idx2 >= span) idx2 -= span;      // q = 2
-        int q = 1;
-        for (; q + 1 < R; q += 2) {
-            acc1 = cadd(acc1, cmul(col[q * qstep], twid<DIR>(tw, idx * tstride)));
-            acc0 = cadd(acc0, cmul(col[(q + 1) * qstep], twid<DIR>(tw, idx2 * tstride)));
-            idx += e2;
-            if (idx >= span) idx -= span;
-            idx2 += e2;
-            if (idx2 >= span) idx2 -= span;
+    if (NS > 1) {
+        for (int item = threadIdx.x; item < n * lines; item += blockDim.x) {
+            const int c = item % lines, o = item / lines;  // o = vt + q nb
+            const int vt = o % nb, q = o / nb;
+            const int m = vt % NS;
+            if (q > 0 && m > 0) {
+                cf* x = src + (size_t)o * lines + c;
+                *x = cmul(*x, twid<DIR>(tw, ((m * q) % span) * tstride));
+            }
         }
-        if (q < R) acc1 = cadd(acc1, cmul(col[q * qstep], twid<DIR>(tw, idx * tstride)));
-        dst[((vt / NS) * span + m + k * NS) * lines + c] = cadd(acc0, acc1);
+        __syncthreads();
+    }
+    const int npair = (R - 1) / 2;
+    const int ngrp = (npair + GP - 1) / GP;
+    const int rstep = n / R;  // W_R^j = tw[j n / R]
+    for (int item = threadIdx.x; item < nb * ngrp * lines; item += blockDim.x) {
+        const int c = item % lines, o = item / lines;
+        const int vt = o % nb, g = o / nb;
+        const int m = vt % NS;
+        const int k0 = 1 + g * GP;
+        const cf* col = src + (size_t)vt * lines + c;
+        const size_t qstep = (size_t)nb * lines;
+        cf x0 = col[0];
+        cf acc0 = x0;  // output 0 (group 0 only)
+        cf ap[GP], am[GP];
+        int idx[GP];
+#pragma unroll
+        for (int j = 0; j < GP; ++j) {
+            ap[j] = x0;
+            am[j] = x0;
+            idx[j] = 0;
+        }
+#pragma unroll ADMM_GUNROLL
+        for (int q = 1; q < R; ++q) {
+            const cf x = col[q * qstep];
+            acc0 = cadd(acc0, x);
+#pragma unroll
+            for (int j = 0; j < GP; ++j) {
+                idx[j] += k0 + j;
+                if (idx[j] >= R) idx[j] -= R;
+                const cf w = twid<DIR>(tw, idx[j] * rstep);
+                const float rr = x.x * w.x, ii = x.y * w.y, ri = x.x * w.y, ir = x.y * w.x;
+                ap[j] = mkc(ap[j].x + (rr - ii), ap[j].y + (ri + ir));  // x w
+                am[j] = mkc(am[j].x + (rr + ii), am[j].y + (ir - ri));  // x conj(w)
+            }
+        }
+        cf* out = dst + ((size_t)(vt / NS) * span + m) * lines + c;
+        const size_t kstep = (size_t)NS * lines;
+        if (g == 0) out[0] = acc0;
+#pragma unroll
+        for (int j = 0; j < GP; ++j) {
+            const int k = k0 + j;
+            if (k <= npair) {
+                out[k * kstep] = ap[j];
+                out[(R - k) * kstep] = am[j];
+            }
+        }
     }
 }
 
 // full transform; data starts in bufA, returns the buffer holding the result
 template <int DIR>
-__device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf* __restrict__ tw) {
+__device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf* __restrict__ tw) {  // bufA is clobbered
     cf* src = bufA;
     cf* dst = bufB;
     int NS = 1;
