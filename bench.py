@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=36, help="CPU baseline sample: timed iterations")
     ap.add_argument("--c5-batch", type=int, default=None, help="C5 only: override the per-GPU batch")
     ap.add_argument("--c5-no-ckpt", action="store_true", help="C5 only: keep all branch activations")
+    ap.add_argument("--c5-channels-last", action="store_true", help="C5 only: NHWC activations (MIOpen NHWC convs)")
+    ap.add_argument("--c5-conv-benchmark", action="store_true", help="C5 only: MIOpen find (cudnn.benchmark)")
     return ap.parse_args()
 
 
@@ -150,6 +152,8 @@ def run_c5(args, world, rank, dev):
     # activations of batch 16 at 512^2 exceed 288 GB -- measured: OOM at 282 GiB allocated)
     if not args.c5_no_ckpt:
         set_branch_checkpointing(model, True)
+    if args.c5_channels_last:
+        model = model.to(memory_format=torch.channels_last)
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
                                                           find_unused_parameters=True)
@@ -157,6 +161,11 @@ def run_c5(args, world, rank, dev):
     y = clean_images(B, C, H, W, seed=CONFIG_SEED + 5 + 1000 * rank, device=dev)
     g = torch.Generator(device=dev).manual_seed(CONFIG_SEED + 5 + rank)
     x = (y + 0.06 * torch.randn(y.shape, generator=g, device=dev)).clamp_(0, 1)
+    if args.c5_conv_benchmark:
+        torch.backends.cudnn.benchmark = True
+    if args.c5_channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+        y = y.contiguous(memory_format=torch.channels_last)
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -211,6 +220,7 @@ def run_c5(args, world, rank, dev):
             "data": "synthetic (piecewise-constant shapes + AWGN 0.06, seeded per rank); random-init weights",
             "config": {"workload": desc, "batch_per_gpu": B, "H": H, "W": W,
                        "branch_checkpointing": not args.c5_no_ckpt,
+                       "channels_last": bool(args.c5_channels_last), "conv_benchmark": bool(args.c5_conv_benchmark),
                        "parallelism": f"ddp{world}" if world > 1 else "single"},
             "admm_share": {"ms_per_step_in_admm_kernels": admm_ms / K, "fraction": admm_ms / 1e3 / T,
                            "launches_per_step": sum(cnt) / K},

@@ -19,7 +19,13 @@ template <class T> __device__ __forceinline__ void st(T* p, T v, bool nt) {
     if (nt) __builtin_nontemporal_store(__builtin_bit_cast(V, v), reinterpret_cast<V*>(p)); else *p = v;
 }
 
-template <int R, bool NT = false>
+template <class T> __device__ __forceinline__ T ld(const T* p, bool nt) {
+    typedef float V __attribute__((ext_vector_type(sizeof(T) / 4)));
+    if (nt) return __builtin_bit_cast(T, __builtin_nontemporal_load(reinterpret_cast<const V*>(p)));
+    return *p;
+}
+
+template <int R, bool NT = false, bool NTL = false>
 __global__ void __launch_bounds__(256) k_mimic(const cf* __restrict__ sp, const cf* __restrict__ uxi,
                                                const cf* __restrict__ uyi, const cf* __restrict__ b,
                                                cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
@@ -32,20 +38,20 @@ __global__ void __launch_bounds__(256) k_mimic(const cf* __restrict__ sp, const 
     const int i0 = (int)(strip % spp) * R;
     const size_t base = (size_t)p * H * N;
     cf acc[E];
-    for (int j = 0; j < E; ++j) acc[j] = sp[base + (size_t)((i0 - 1 + H) & (H - 1)) * N + t + L * j];
+    for (int j = 0; j < E; ++j) acc[j] = ld(&sp[base + (size_t)((i0 - 1 + H) & (H - 1)) * N + t + L * j], NTL);
     for (int rr = 0; rr <= R; ++rr) {
         const size_t ro = base + (size_t)((i0 + rr) & (H - 1)) * N;
         const size_t rm = base + (size_t)((i0 + rr - 1 + H) & (H - 1)) * N;
         cf x[E], uy[E];
-        for (int j = 0; j < E; ++j) x[j] = sp[ro + t + L * j];
-        for (int j = 0; j < E; ++j) { uy[j] = uyi[ro + t + L * j]; uy[j].x += x[j].x; uy[j].y += acc[j].y; }
+        for (int j = 0; j < E; ++j) x[j] = ld(&sp[ro + t + L * j], NTL);
+        for (int j = 0; j < E; ++j) { uy[j] = ld(&uyi[ro + t + L * j], NTL); uy[j].x += x[j].x; uy[j].y += acc[j].y; }
         if (rr < R) for (int j = 0; j < E; ++j) st(&uyo[ro + t + L * j], uy[j], NT);
         if (rr >= 1) {
-            for (int j = 0; j < E; ++j) { cf bb = b[rm + t + L * j]; acc[j].x += bb.x; acc[j].y -= bb.y; }
+            for (int j = 0; j < E; ++j) { cf bb = ld(&b[rm + t + L * j], NTL); acc[j].x += bb.x; acc[j].y -= bb.y; }
             for (int j = 0; j < E; ++j) st(&so[rm + t + L * j], acc[j], NT);
         }
         if (rr < R) {
-            for (int j = 0; j < E; ++j) { cf u = uxi[ro + t + L * j]; u.x -= x[j].y; u.y += x[j].x; st(&uxo[ro + t + L * j], u, NT); }
+            for (int j = 0; j < E; ++j) { cf u = ld(&uxi[ro + t + L * j], NTL); u.x -= x[j].y; u.y += x[j].x; st(&uxo[ro + t + L * j], u, NT); }
         }
         for (int j = 0; j < E; ++j) acc[j] = x[j];
     }
@@ -398,6 +404,20 @@ int main() {
             const double bytes = 9.0 * arr * ITERS;  // 36 B/px per iteration = 9 cf-arrays of 8 B per 2 px
             printf("chunk %3d planes (%6.1f MiB live): %8.2f ms for %d it  -> %6.0f GB/s algorithmic, %6.1f it/s\n",
                    Pc, Pc * pn * sizeof(cf) * 7 / 1048576.0, ms, ITERS, bytes / (ms * 1e-3) / 1e9, ITERS / (ms * 1e-3));
+        }
+        return 0;
+    }
+    if (getenv("NT_ONLY")) {  // cache-policy ceilings of pass A's pattern
+        const long long ns = (long long)P * H / 8;
+        auto m = [&](auto kern, const char* name) {
+            timeit(name, 7 * arr, [&] { kern<<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+        };
+        for (int rep = 0; rep < 2; ++rep) {
+            timeit("copy float2 1/thread", 2 * arr, [&] { k_copy2<false><<<(unsigned)(n / 256), 256>>>((const float2*)buf[0], (float2*)buf[1]); });
+            timeit("copy float2 1/thread nt", 2 * arr, [&] { k_copy2<true><<<(unsigned)(n / 256), 256>>>((const float2*)buf[0], (float2*)buf[1]); });
+            m(k_mimic<8, false, false>, "mimic R=8 plain");
+            m(k_mimic<8, true, false>, "mimic R=8 nt stores");
+            m(k_mimic<8, true, true>, "mimic R=8 nt stores + loads");
         }
         return 0;
     }
