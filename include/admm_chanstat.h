@@ -68,6 +68,18 @@ int admm_chanstat_pool_depth(int dtype, const void* x, int64_t B, int64_t C, int
 int admm_chanstat_pool_backward(int dtype, const void* x, const void* out, const int16_t* idx, const void* gout,
                                 int64_t B, int64_t C, int64_t HW, void* gx, void* stream);
 
+/* ---- whole-plane median and mode (ChannelWiseAttention's amedian / amodes, reference
+ * elayers/cwa.py: x.view(B, C, -1).median(-1) / .mode(-1)), 16-bit types only.
+ * x          : [P][N] elements of `dtype` (ADMM_CHANSTAT_BF16 or _F16)
+ * median_idx : [P] int64, flat index of torch.median's (CPU) element, or NULL
+ * mode_idx   : [P] int64, flat index of torch.mode's (CPU) element, or NULL
+ * ws         : device workspace of admm_planestat_workspace_size(P, N) bytes (32 N B per plane)
+ * depth_limit: -1 (std::sort's 2*floor(log2 N)); >= 0 forces the introsort depth budget (tests)
+ * Values are x at those indices; semantics as ChannelPool's median / mode above. */
+int admm_planestat_workspace_size(int64_t P, int64_t N, size_t* bytes);
+int admm_planestat_median_mode(int dtype, const void* x, int64_t P, int64_t N, int64_t* median_idx,
+                               int64_t* mode_idx, void* ws, size_t ws_bytes, int depth_limit, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

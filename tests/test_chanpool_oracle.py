@@ -111,7 +111,7 @@ def test_depth_limited_sort_still_sorts():
 
 def _declared():
     txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
-    return sorted(set(re.findall(r"\b(admm_chanstat_\w+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(admm_(?:chanstat|planestat)_\w+)\s*\(", txt)))
 
 
 def test_chanstat_header_binding_and_exports():
@@ -119,7 +119,7 @@ def test_chanstat_header_binding_and_exports():
     assert _declared() == sorted(_native.EXPORTED_CHANSTAT)
     so = _native.lib_path()
     out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
-    assert set(_declared()) <= set(re.findall(r"\sT\s(admm_chanstat_\w+)", out))
+    assert set(_declared()) <= set(re.findall(r"\sT\s(admm_(?:chanstat|planestat)_\w+)", out))
     lib = _native.load()
     assert lib.admm_chanstat_max_channels(_native.CHANSTAT_F32) == 128
     assert lib.admm_chanstat_max_channels(_native.CHANSTAT_BF16) == 256
@@ -130,6 +130,16 @@ def test_chanstat_header_binding_and_exports():
     assert lib.admm_chanstat_pool(_native.CHANSTAT_F32, 8, 1, 129, 4, 8, None, None) == _native.ADMM_TV_EUNSUPPORTED
     assert lib.admm_chanstat_pool(_native.CHANSTAT_BF16, 8, 0, 86, 4, 8, None, None) == 0  # empty batch: no launch
     assert lib.admm_chanstat_pool_depth(_native.CHANSTAT_BF16, 8, 1, 86, 4, 8, None, 17, None) == _native.ADMM_TV_EINVAL
+    import ctypes
+    n = ctypes.c_size_t(0)
+    assert lib.admm_planestat_workspace_size(1376, 512 * 512, ctypes.byref(n)) == 0
+    assert n.value >= 1376 * 32 * 512 * 512
+    # plane statistics: fp32 unsupported (16-bit codes only), workspace checked before any launch
+    assert lib.admm_planestat_median_mode(_native.CHANSTAT_F32, 8, 2, 16, None, None, 8, 1 << 20, -1, None) \
+        == _native.ADMM_TV_EUNSUPPORTED
+    assert lib.admm_planestat_median_mode(_native.CHANSTAT_BF16, 8, 2, 16, None, None, 8, 16, -1, None) \
+        == _native.ADMM_TV_EWORKSPACE
+    assert lib.admm_planestat_median_mode(_native.CHANSTAT_BF16, 8, 0, 16, None, None, None, 0, -1, None) == 0
 
 
 def test_channel_pool_module_cpu_is_reference_ops():

@@ -5,20 +5,87 @@ compress_weight.{i}):
 
   weights = sum_m  w_m * stat_m(x)          per (b, c), stats over the whole plane    cwa.py:73-77
   out     = x * sigmoid(conv2(conv1(x)) * weights)                                    cwa.py:79-84
+
+The per-plane median and mode run as HIP kernels on the GPU for 16-bit inputs
+(include/admm_chanstat.h, csrc/plane_stats.hip) with the reference's CPU tie rules; PyTorch's
+GPU median/mode over 512^2 planes are per-slice thrust sorts (thousands of launches per step).
+CPU tensors and fp32/fp64 inputs take the reference's op sequence.
 """
+import os
+
 import torch
 import torch.nn as nn
+
+_PLANE_DTYPES = {torch.bfloat16: 1, torch.float16: 2}
 
 
 def _planes(x: torch.Tensor) -> torch.Tensor:
     return x.reshape(x.shape[0], x.shape[1], -1)
 
 
+def plane_select_native(x: torch.Tensor, which: str, depth_limit=None) -> torch.Tensor:
+    """(B, C, H, W) ROCm bf16/fp16 tensor -> (B*C,) int64 flat indices of torch.median's ("median")
+    or torch.mode's ("mode") element of each plane, by the HIP kernels."""
+    from .. import _native
+    import ctypes
+    lib = _native.load()
+    xs = _planes(x).contiguous()
+    P, N = xs.shape[0] * xs.shape[1], xs.shape[2]
+    idx = torch.empty(P, dtype=torch.int64, device=x.device)
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    # planes per call: workspace (32 N bytes per plane) kept near 1 GiB
+    chunk = max(1, min(P, (1 << 30) // max(1, 32 * N)))
+    nb = ctypes.c_size_t(0)
+    _native.check(lib.admm_planestat_workspace_size(chunk, N, ctypes.byref(nb)))
+    ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device)
+    flat = xs.reshape(P, N)
+    for p0 in range(0, P, chunk):
+        n = min(chunk, P - p0)
+        out = idx[p0:p0 + n].data_ptr()
+        _native.check(lib.admm_planestat_median_mode(
+            _PLANE_DTYPES[x.dtype], flat[p0].data_ptr(), n, N, out if which == "median" else None,
+            out if which == "mode" else None, ws.data_ptr(), ws.numel(),
+            -1 if depth_limit is None else int(depth_limit), stream))
+    return idx
+
+
+class _PlaneSelect(torch.autograd.Function):
+    """value of each plane at the selected flat index; the gradient goes to that element
+    (the reference's value_selecting_reduction_backward)."""
+
+    @staticmethod
+    def forward(ctx, x, which):
+        idx = plane_select_native(x, which)
+        B, C = x.shape[0], x.shape[1]
+        flat = _planes(x).reshape(B * C, -1)
+        ctx.save_for_backward(idx)
+        ctx.shape = x.shape
+        return flat.gather(1, idx[:, None]).reshape(B, C)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        B, C = ctx.shape[0], ctx.shape[1]
+        gx = torch.zeros((B * C, ctx.shape[2] * ctx.shape[3]), dtype=g.dtype,
+                         device=g.device)
+        gx.scatter_(1, idx[:, None], g.reshape(B * C, 1))
+        return gx.reshape(ctx.shape), None
+
+
+def _native_plane_applies(x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.dtype in _PLANE_DTYPES and x.shape[2] * x.shape[3] > 0
+            and os.environ.get("ADMMTOR_PLANESTAT") != "torch")
+
+
 def amedian(x):
+    if _native_plane_applies(x):
+        return _PlaneSelect.apply(x, "median")
     return _planes(x).median(dim=-1).values
 
 
 def amodes(x):
+    if _native_plane_applies(x):
+        return _PlaneSelect.apply(x, "mode")
     return _planes(x).mode(dim=-1).values
 
 
