@@ -73,7 +73,7 @@ int admm_chanstat_pool_backward(int dtype, const void* x, const void* out, const
  * x          : [P][N] elements of `dtype` (ADMM_CHANSTAT_BF16 or _F16)
  * median_idx : [P] int64, flat index of torch.median's (CPU) element, or NULL
  * mode_idx   : [P] int64, flat index of torch.mode's (CPU) element, or NULL
- * ws         : device workspace of admm_planestat_workspace_size(P, N) bytes (32 N B per plane)
+ * ws         : device workspace of admm_planestat_workspace_size(P, N) bytes (24 N B per plane)
  * depth_limit: -1 (std::sort's 2*floor(log2 N)); >= 0 forces the introsort depth budget (tests)
  * Values are x at those indices; semantics as ChannelPool's median / mode above. */
 int admm_planestat_workspace_size(int64_t P, int64_t N, size_t* bytes);

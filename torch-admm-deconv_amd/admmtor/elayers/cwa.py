@@ -33,8 +33,11 @@ def plane_select_native(x: torch.Tensor, which: str, depth_limit=None) -> torch.
     P, N = xs.shape[0] * xs.shape[1], xs.shape[2]
     idx = torch.empty(P, dtype=torch.int64, device=x.device)
     stream = torch.cuda.current_stream(x.device).cuda_stream
-    # planes per call: workspace (32 N bytes per plane) kept near 1 GiB
-    chunk = max(1, min(P, (1 << 30) // max(1, 32 * N)))
+    # planes per call: workspace (24 N bytes per plane) up to 8 GiB, calls balanced (each call
+    # should cover the chip: one workgroup per plane)
+    most = max(1, (8 << 30) // max(1, 24 * N))
+    ncall = -(-P // most)
+    chunk = -(-P // ncall)
     nb = ctypes.c_size_t(0)
     _native.check(lib.admm_planestat_workspace_size(chunk, N, ctypes.byref(nb)))
     ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device)

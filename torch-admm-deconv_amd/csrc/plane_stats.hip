@@ -9,13 +9,13 @@
 //    code space per pass (32768 x u32 = 128 KB); gives the median's code and its rank within its
 //    run of equal values, and the mode (smallest most frequent code).
 //  * k_plane_median_idx: the r-th occurrence of the median's code in flat order (torch.median's
-//    stable rank), by block-wide prefix counts over rows of 1024 elements.
+//    stable rank), by block-wide prefix counts over steps of 8192 elements.
 //  * k_plane_mode_idx: the index torch.mode (CPU) reports is where libstdc++ std::sort leaves the
 //    last element of the mode's run.  Only the rightmost partition range still holding a
 //    mode-valued element matters, and only while it holds two or more (ranges keep their order,
 //    the final insertion sort is stable), so the kernel replays the partitions along that one
 //    path: each Hoare partition as four passes over the range (stop counts, stop ranks and the
-//    swap count S, swapped elements into slots, the partitioned range into the other buffer).
+//    swap count S, swapped elements into slots, swapped positions updated in place).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -27,6 +27,7 @@ namespace {
 
 constexpr int NT = 1024;  // threads per workgroup (16 waves)
 constexpr int NW = NT / 64;
+constexpr int KR = 8;      // elements per thread per block-scan step of the partition replay
 
 __device__ __forceinline__ uint32_t ord16_bf16(uint32_t u) {
     if ((u & 0x7F80u) == 0x7F80u && (u & 0x7Fu)) return 0xFFFFu;  // NaN above +inf
@@ -42,36 +43,40 @@ template <int DT> __device__ __forceinline__ uint32_t code_of(uint16_t raw) {
     return DT == ADMM_CHANSTAT_BF16 ? ord16_bf16(raw) : ord16_f16(raw);
 }
 
-__device__ __forceinline__ int mbcnt(uint64_t m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// block-wide exclusive ranks of two flags in one row of NT elements (one per thread); returns the
-// row totals.  Two barriers; `sh` holds 2 * NW ints.
-__device__ __forceinline__ void row_rank2(bool a, bool b, int* sh, int& ra, int& rb, int& ta, int& tb) {
+// block-wide exclusive prefix sums of two per-thread counts (thread order); row totals.  Two
+// barriers; `sh` holds 2 * NW ints.
+__device__ __forceinline__ void block_scan2(int a, int b, int* sh, int& ea, int& eb, int& ta, int& tb) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t ma = __ballot(a), mb = __ballot(b);
-    if (lane == 0) {
-        sh[w] = __popcll(ma);
-        sh[NW + w] = __popcll(mb);
+    int ia = a, ib = b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int ua = __shfl_up(ia, o), ub = __shfl_up(ib, o);
+        if (lane >= o) {
+            ia += ua;
+            ib += ub;
+        }
+    }
+    if (lane == 63) {
+        sh[w] = ia;
+        sh[NW + w] = ib;
     }
     __syncthreads();
-    int ba = 0, bb = 0;
+    int oa = 0, ob = 0;
     ta = 0;
     tb = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
         const int ca = sh[i], cb = sh[NW + i];
         if (i < w) {
-            ba += ca;
-            bb += cb;
+            oa += ca;
+            ob += cb;
         }
         ta += ca;
         tb += cb;
     }
     __syncthreads();
-    ra = ba + mbcnt(ma);
-    rb = bb + mbcnt(mb);
+    ea = oa + ia - a;
+    eb = ob + ib - b;
 }
 
 __device__ __forceinline__ int block_sum(int v, int* sh) {
@@ -109,6 +114,7 @@ __global__ void __launch_bounds__(NT) k_plane_hist(const uint16_t* __restrict__ 
     for (int half = 0; half < 2; ++half) {
         for (int i = t; i < 32768; i += NT) hist[i] = 0u;
         __syncthreads();
+#pragma unroll 8
         for (long long i = t; i < N; i += NT) {
             const uint32_t c = code_of<DT>(xp[i]);
             if ((int)(c >> 15) == half) atomicAdd(&hist[c & 0x7FFFu], 1u);
@@ -197,12 +203,27 @@ __global__ void __launch_bounds__(NT) k_plane_median_idx(const uint16_t* __restr
     int r = st[blockIdx.x].med_r;
     if (t == 0) found = -1;
     __syncthreads();
-    for (long long base = 0; base < N; base += NT) {
-        const long long i = base + t;
-        const bool f = i < N && code_of<DT>(xp[i]) == mc;
-        int rk, d0, tot, d1;
-        row_rank2(f, false, sh, rk, d0, tot, d1);
-        if (f && rk == r) found = i;
+    for (long long base = 0; base < N; base += (long long)NT * KR) {
+        const long long i0 = base + (long long)t * KR;
+        bool f[KR];
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < KR; ++j) {
+            f[j] = i0 + j < N && code_of<DT>(xp[i0 + j]) == mc;
+            n += f[j] ? 1 : 0;
+        }
+        int ex, d0, tot, d1;
+        block_scan2(n, 0, sh, ex, d0, tot, d1);
+        if (r >= ex && r < ex + n) {  // this thread holds the r-th occurrence
+            int k = r - ex;
+#pragma unroll
+            for (int j = 0; j < KR; ++j) {
+                if (f[j]) {
+                    if (k == 0) found = i0 + j;
+                    --k;
+                }
+            }
+        }
         r -= tot;
         if (r < 0) break;  // uniform
     }
@@ -264,10 +285,9 @@ __global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restric
     const uint16_t* xp = x + (size_t)blockIdx.x * N;
     const PlaneStat s = st[blockIdx.x];
     const uint32_t m = (uint32_t)s.mode_code;
-    // per plane: cur, nxt, slots (L then R) as u64 [N] each, ranks int2 [N]
-    unsigned long long* cur = ws + (size_t)blockIdx.x * 4 * N;
-    unsigned long long* nxt = cur + N;
-    unsigned long long* slotL = nxt + N;
+    // per plane: the working array and the swap slots (L then R) as u64 [N] each, ranks int2 [N]
+    unsigned long long* cur = ws + (size_t)blockIdx.x * 3 * N;
+    unsigned long long* slotL = cur + N;
     unsigned long long* slotR = slotL + (N + 1) / 2;
     int2* rk = reinterpret_cast<int2*>(slotL + N);
 
@@ -283,6 +303,7 @@ __global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restric
         if (t == 0) idx[blockIdx.x] = (long long)lastp1 - 1;
         return;
     }
+#pragma unroll 8
     for (long long i = t; i < N; i += NT) cur[i] = ((unsigned long long)code_of<DT>(xp[i]) << 32) | (unsigned long long)i;
     __syncthreads();
 
@@ -295,6 +316,7 @@ __global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restric
         if (t == 0) sh_u[0] = 0;  // last position + 1
         __syncthreads();
         int cnt = 0;
+#pragma unroll 8
         for (long long p = f + t; p < l; p += NT) {
             if (ecode(cur[p]) == m) {
                 ++cnt;
@@ -313,7 +335,8 @@ __global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restric
             __syncthreads();
             if (t == 0) sh_u[0] = 0;
             __syncthreads();
-            for (long long p = f + t; p < l; p += NT)
+    #pragma unroll 8
+        for (long long p = f + t; p < l; p += NT)
                 if (ecode(cur[p]) == m) atomicMax(&sh_u[0], (unsigned long long)(p + 1));
             __syncthreads();
             answer = (long long)(cur[(long long)sh_u[0] - 1] & 0xFFFFFFFFull);
@@ -337,23 +360,41 @@ __global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restric
         const uint32_t pv = ecode(sh_e[0]);
         // pass 1: right-stop count over [f + 1, l)
         int cl = 0;
+#pragma unroll 8
         for (long long p = f + 1 + t; p < l; p += NT) cl += ecode(cur[p]) <= pv;
         const int TL = block_sum(cl, sh);
-        // pass 2: ranks (left stops from the left, right stops from the right) and the swap count
+        // pass 2: ranks (left stops from the left, right stops from the right) and the swap count;
+        // each thread takes KR consecutive elements per step (one block scan per NT * KR elements)
         int sw = 0;
         {
             int gb = 0, lb = 0;
-            for (long long base = f + 1; base < l; base += NT) {
-                const long long p = base + t;
-                const bool in = p < l;
-                const uint32_t c = in ? ecode(cur[p]) : 0u;
-                const bool ge = in && c >= pv, le = in && c <= pv;
-                int rg, rl, tg, tl;
-                row_rank2(ge, le, sh, rg, rl, tg, tl);
-                const int lrank = gb + rg;
-                const int rrank = TL - (lb + rl + (le ? 1 : 0));  // right stops after p
-                if (in) rk[p] = make_int2(ge ? lrank : -1, le ? rrank : -1);
-                sw += (ge && lrank < rrank) ? 1 : 0;
+            for (long long base = f + 1; base < l; base += (long long)NT * KR) {
+                const long long p0 = base + (long long)t * KR;
+                uint32_t c[KR];
+                int ng = 0, nl = 0;
+#pragma unroll
+                for (int j = 0; j < KR; ++j) {
+                    const bool in = p0 + j < l;
+                    c[j] = in ? ecode(cur[p0 + j]) : 0u;
+                    ng += (in && c[j] >= pv) ? 1 : 0;
+                    nl += (in && c[j] <= pv) ? 1 : 0;
+                }
+                int eg, el, tg, tl;
+                block_scan2(ng, nl, sh, eg, el, tg, tl);
+                int rg = gb + eg, rl = lb + el;
+#pragma unroll
+                for (int j = 0; j < KR; ++j) {
+                    const long long p = p0 + j;
+                    if (p < l) {
+                        const bool ge = c[j] >= pv, le = c[j] <= pv;
+                        const int lrank = rg;
+                        const int rrank = TL - (rl + (le ? 1 : 0));  // right stops after p
+                        rk[p] = make_int2(ge ? lrank : -1, le ? rrank : -1);
+                        sw += (ge && lrank < rrank) ? 1 : 0;
+                        rg += ge ? 1 : 0;
+                        rl += le ? 1 : 0;
+                    }
+                }
                 gb += tg;
                 lb += tl;
             }
@@ -365,6 +406,7 @@ __global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restric
             sh_l[2] = l;          // R_S (l when S == 0)
         }
         __syncthreads();
+#pragma unroll 8
         for (long long p = f + 1 + t; p < l; p += NT) {
             const int2 r = rk[p];
             if (r.x >= 0 && r.x < S) slotL[r.x] = cur[p];
@@ -375,23 +417,26 @@ __global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restric
         __threadfence_block();
         __syncthreads();
         const long long cut = min(sh_l[1], sh_l[2]);
-        // pass 4: the partitioned range into nxt; mode-valued elements right of the cut?
+        // pass 4: the swapped positions take their partners (in place: every other position keeps
+        // its element); mode-valued elements right of the cut?
         int mr = 0;
-        for (long long p = f + t; p < l; p += NT) {
-            unsigned long long e = cur[p];
-            if (p > f) {
-                const int2 r = rk[p];
-                if (r.x >= 0 && r.x < S) e = slotR[r.x];
-                else if (r.y >= 0 && r.y < S) e = slotL[r.y];
+#pragma unroll 8
+        for (long long p = f + 1 + t; p < l; p += NT) {
+            const int2 r = rk[p];
+            unsigned long long e;
+            if (r.x >= 0 && r.x < S) {
+                e = slotR[r.x];
+                cur[p] = e;
+            } else if (r.y >= 0 && r.y < S) {
+                e = slotL[r.y];
+                cur[p] = e;
+            } else {
+                e = cur[p];
             }
-            nxt[p] = e;
             mr += (p >= cut && ecode(e) == m) ? 1 : 0;
         }
         const int mright = block_sum(mr, sh);
         __threadfence_block();
-        unsigned long long* tmp = cur;
-        cur = nxt;
-        nxt = tmp;
         if (mright > 0) f = cut;
         else l = cut;
     }
@@ -404,7 +449,7 @@ extern "C" {
 
 int admm_planestat_workspace_size(int64_t P, int64_t N, size_t* bytes) {
     if (!bytes || P < 0 || N < 0) return ADMM_TV_EINVAL;
-    *bytes = (size_t)P * (sizeof(PlaneStat) + (size_t)4 * N * sizeof(unsigned long long)) + 256;
+    *bytes = (size_t)P * (sizeof(PlaneStat) + (size_t)3 * N * sizeof(unsigned long long)) + 256;
     return 0;
 }
 
