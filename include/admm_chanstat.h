@@ -80,6 +80,14 @@ int admm_planestat_workspace_size(int64_t P, int64_t N, size_t* bytes);
 int admm_planestat_median_mode(int dtype, const void* x, int64_t P, int64_t N, int64_t* median_idx,
                                int64_t* mode_idx, void* ws, size_t ws_bytes, int depth_limit, void* stream);
 
+/* The same selection for any of the three dtypes (fp32 included) from per-plane statistics the
+ * caller computed (e.g. from a segmented sort): stats[P][4] int32 = {mode code, mode count,
+ * median code, rank of the median within its run of equal values}, codes being the
+ * order-preserving unsigned images of the value bits (-0 folded onto +0, NaN the all-ones code;
+ * 32-bit codes stored as their int32 bit patterns). */
+int admm_planestat_select(int dtype, const void* x, int64_t P, int64_t N, const int32_t* stats, int64_t* median_idx,
+                          int64_t* mode_idx, void* ws, size_t ws_bytes, int depth_limit, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,7 +20,7 @@ def _inputs(shape, dt, kind, seed):
     return (torch.randint(-k, k + 1, shape, generator=g).double() / 8).to(dt)
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("shape", [(2, 3, 3, 3), (1, 2, 4, 4), (2, 3, 17, 31), (2, 4, 64, 64), (1, 3, 256, 256)])
 def test_median_mode_vs_torch_cpu(cuda_dev, dt, shape):
     from admmtor.elayers.cwa import plane_select_native
@@ -45,20 +45,22 @@ def test_unique_values_and_small_planes(cuda_dev):
     assert plane_select_native(x1.to(cuda_dev), "mode").item() == 0
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("depth", [0, 1, 3])
-def test_depth_limited_vs_oracle(cuda_dev, depth):
+def test_depth_limited_vs_oracle(cuda_dev, depth, dt):
     from admmtor.elayers.cwa import plane_select_native
-    x = _inputs((1, 2, 20, 30), torch.bfloat16, "few", 7 + depth)
+    x = _inputs((1, 2, 20, 30), dt, "few", 7 + depth)
     got = plane_select_native(x.to(cuda_dev), "mode", depth_limit=depth).cpu().numpy()
     for p in range(2):
         col = x.reshape(2, -1)[p].double().numpy()
         assert got[p] == mode_of(col, depth_limit=depth)[1]
 
 
-def test_gradient_vs_torch_cpu(cuda_dev):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_gradient_vs_torch_cpu(cuda_dev, dt):
     from admmtor.elayers.cwa import amedian, amodes
-    x = _inputs((2, 3, 32, 32), torch.bfloat16, "many", 11)
-    w = torch.randn(2, 3, generator=torch.Generator().manual_seed(12)).to(torch.bfloat16)
+    x = _inputs((2, 3, 32, 32), dt, "many", 11)
+    w = torch.randn(2, 3, generator=torch.Generator().manual_seed(12)).to(dt)
     xg = x.to(cuda_dev).requires_grad_(True)
     (amedian(xg) * w.to(cuda_dev) + amodes(xg) * 2 * w.to(cuda_dev)).sum().backward()
     xc = x.clone().requires_grad_(True)

@@ -26,11 +26,12 @@ def timed(fn, n):
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    for B, C, H, W in ((16, 86, 512, 512), (16, 86, 128, 128)):
-        x = torch.randn((B, C, H, W), device=dev, generator=g).to(torch.bfloat16)
+    for B, C, H, W, dt in ((16, 86, 512, 512, torch.bfloat16), (16, 86, 128, 128, torch.bfloat16),
+                           (16, 86, 512, 512, torch.float32)):
+        x = torch.randn((B, C, H, W), device=dev, generator=g).to(dt)
         med = timed(lambda: plane_select_native(x, "median"), 5)
         mod = timed(lambda: plane_select_native(x, "mode"), 5)
-        line = f"{B}x{C}x{H}x{W} bf16: native median {med:.2f} ms, mode {mod:.2f} ms"
+        line = f"{B}x{C}x{H}x{W} {str(dt)[6:]}: native median {med:.2f} ms, mode {mod:.2f} ms"
         if "--native-only" not in sys.argv:
             f = x.reshape(B, C, -1)
             tmed = timed(lambda: f.median(dim=-1), 1)

@@ -45,6 +45,7 @@ EXPORTED_CHANSTAT = (
     "admm_chanstat_pool_backward",
     "admm_planestat_workspace_size",
     "admm_planestat_median_mode",
+    "admm_planestat_select",
 )
 CHANSTAT_F32, CHANSTAT_BF16, CHANSTAT_F16 = 0, 1, 2
 
@@ -142,6 +143,8 @@ def load() -> ctypes.CDLL:
         L.admm_planestat_workspace_size.argtypes = [i64, i64, ctypes.POINTER(sz)]
         L.admm_planestat_median_mode.restype = ctypes.c_int
         L.admm_planestat_median_mode.argtypes = [ctypes.c_int, vp, i64, i64, vp, vp, vp, sz, ctypes.c_int, vp]
+        L.admm_planestat_select.restype = ctypes.c_int
+        L.admm_planestat_select.argtypes = [ctypes.c_int, vp, i64, i64, vp, vp, vp, vp, sz, ctypes.c_int, vp]
         if L.admm_tv_abi_version() != ABI_VERSION:
             raise ImportError("admmtor: native library ABI version mismatch")
         _lib = L

@@ -6,26 +6,64 @@ compress_weight.{i}):
   weights = sum_m  w_m * stat_m(x)          per (b, c), stats over the whole plane    cwa.py:73-77
   out     = x * sigmoid(conv2(conv1(x)) * weights)                                    cwa.py:79-84
 
-The per-plane median and mode run as HIP kernels on the GPU for 16-bit inputs
-(include/admm_chanstat.h, csrc/plane_stats.hip) with the reference's CPU tie rules; PyTorch's
-GPU median/mode over 512^2 planes are per-slice thrust sorts (thousands of launches per step).
-CPU tensors and fp32/fp64 inputs take the reference's op sequence.
+The per-plane median and mode run as HIP kernels on the GPU (include/admm_chanstat.h,
+csrc/plane_stats.hip) with the reference's CPU tie rules; PyTorch's GPU median/mode over 512^2
+planes are per-slice thrust sorts (thousands of launches per step).  16-bit inputs get their
+value statistics from an LDS histogram, fp32 from one segmented sort; CPU tensors and fp64 take
+the reference's op sequence.
 """
 import os
 
 import torch
 import torch.nn as nn
 
-_PLANE_DTYPES = {torch.bfloat16: 1, torch.float16: 2}
+_PLANE_DTYPES = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
 
 
 def _planes(x: torch.Tensor) -> torch.Tensor:
     return x.reshape(x.shape[0], x.shape[1], -1)
 
 
+def _ord32(v: torch.Tensor) -> torch.Tensor:
+    """Order-preserving unsigned image of fp32 bits (-0 -> +0, NaN -> all ones), as int64."""
+    b = v.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    mag = b & 0x7FFFFFFF
+    b = torch.where(mag == 0, torch.zeros_like(b), b)
+    o = torch.where((b & 0x80000000) != 0, (~b) & 0xFFFFFFFF, b | 0x80000000)
+    return torch.where(mag > 0x7F800000, torch.full_like(o, 0xFFFFFFFF), o)
+
+
+def _plane_stats_f32(flat: torch.Tensor, which: str) -> torch.Tensor:
+    """(P, N) fp32 -> (P, 4) int32 {mode code, mode count, median code, median rank in its run}
+    (the 16-bit types get these from the kernels' LDS histogram).  median: the value from
+    torch's median, its rank from a count of smaller values; mode: runs of one segmented sort."""
+    P, N = flat.shape
+    st = torch.zeros((P, 4), dtype=torch.int64, device=flat.device)
+    if which == "median":
+        vm = flat.median(dim=1).values
+        st[:, 2] = _ord32(vm)
+        st[:, 3] = (N - 1) // 2 - (flat < vm[:, None]).sum(dim=1)
+    else:
+        sv = torch.sort(flat, dim=1).values
+        start = torch.ones((P, N), dtype=torch.bool, device=flat.device)
+        start[:, 1:] = sv[:, 1:] != sv[:, :-1]
+        pos = torch.arange(N, device=flat.device, dtype=torch.int32).expand(P, N)
+        # next run start after each position (N past the last), by a reversed running minimum
+        nxt = torch.full((P, N), N, device=flat.device, dtype=torch.int32)
+        nxt[:, :-1] = torch.where(start[:, 1:], pos[:, 1:], nxt[:, 1:])
+        nxt = torch.flip(torch.cummin(torch.flip(nxt, [1]), dim=1).values, [1])
+        length = torch.where(start, nxt - pos, torch.zeros_like(pos))
+        mcount = length.max(dim=1).values
+        first = torch.argmax((length == mcount[:, None]).to(torch.int8), dim=1)  # first longest run
+        st[:, 0] = _ord32(sv.gather(1, first[:, None]).squeeze(1))
+        st[:, 1] = mcount.to(torch.int64)
+    st = torch.where(st >= 2 ** 31, st - 2 ** 32, st)  # 32-bit codes as int32 bit patterns
+    return st.to(torch.int32).contiguous()
+
+
 def plane_select_native(x: torch.Tensor, which: str, depth_limit=None) -> torch.Tensor:
-    """(B, C, H, W) ROCm bf16/fp16 tensor -> (B*C,) int64 flat indices of torch.median's ("median")
-    or torch.mode's ("mode") element of each plane, by the HIP kernels."""
+    """(B, C, H, W) ROCm bf16/fp16/fp32 tensor -> (B*C,) int64 flat indices of torch.median's
+    ("median") or torch.mode's ("mode") element of each plane, by the HIP kernels."""
     from .. import _native
     import ctypes
     lib = _native.load()
@@ -45,10 +83,16 @@ def plane_select_native(x: torch.Tensor, which: str, depth_limit=None) -> torch.
     for p0 in range(0, P, chunk):
         n = min(chunk, P - p0)
         out = idx[p0:p0 + n].data_ptr()
-        _native.check(lib.admm_planestat_median_mode(
-            _PLANE_DTYPES[x.dtype], flat[p0].data_ptr(), n, N, out if which == "median" else None,
-            out if which == "mode" else None, ws.data_ptr(), ws.numel(),
-            -1 if depth_limit is None else int(depth_limit), stream))
+        dl = -1 if depth_limit is None else int(depth_limit)
+        if x.dtype == torch.float32:
+            st = _plane_stats_f32(flat[p0:p0 + n], which)
+            _native.check(lib.admm_planestat_select(
+                0, flat[p0].data_ptr(), n, N, st.data_ptr(), out if which == "median" else None,
+                out if which == "mode" else None, ws.data_ptr(), ws.numel(), dl, stream))
+        else:
+            _native.check(lib.admm_planestat_median_mode(
+                _PLANE_DTYPES[x.dtype], flat[p0].data_ptr(), n, N, out if which == "median" else None,
+                out if which == "mode" else None, ws.data_ptr(), ws.numel(), dl, stream))
     return idx
 
 

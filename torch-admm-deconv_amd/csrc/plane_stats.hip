@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "admm_chanstat.h"
 #include "admm_tv.h"
@@ -39,8 +40,17 @@ __device__ __forceinline__ uint32_t ord16_f16(uint32_t u) {
     if ((u & 0x7FFFu) == 0) u = 0;
     return (u & 0x8000u) ? (~u & 0xFFFFu) : (u | 0x8000u);
 }
-template <int DT> __device__ __forceinline__ uint32_t code_of(uint16_t raw) {
-    return DT == ADMM_CHANSTAT_BF16 ? ord16_bf16(raw) : ord16_f16(raw);
+__device__ __forceinline__ uint32_t ord32_f32(uint32_t u) {
+    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return 0xFFFFFFFFu;
+    if ((u & 0x7FFFFFFFu) == 0) u = 0;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+template <int DT> struct Elem { using type = uint16_t; };
+template <> struct Elem<ADMM_CHANSTAT_F32> { using type = uint32_t; };
+template <int DT> __device__ __forceinline__ uint32_t code_of(typename Elem<DT>::type raw) {
+    if constexpr (DT == ADMM_CHANSTAT_F32) return ord32_f32(raw);
+    else if constexpr (DT == ADMM_CHANSTAT_BF16) return ord16_bf16(raw);
+    else return ord16_f16(raw);
 }
 
 // block-wide exclusive prefix sums of two per-thread counts (thread order); row totals.  Two
@@ -193,12 +203,12 @@ __global__ void __launch_bounds__(NT) k_plane_hist(const uint16_t* __restrict__ 
 
 // --------------------------------------------------------------------------- median index
 template <int DT>
-__global__ void __launch_bounds__(NT) k_plane_median_idx(const uint16_t* __restrict__ x, long long N,
+__global__ void __launch_bounds__(NT) k_plane_median_idx(const typename Elem<DT>::type* __restrict__ x, long long N,
                                                         const PlaneStat* __restrict__ st, int64_t* __restrict__ idx) {
     __shared__ int sh[2 * NW];
     __shared__ long long found;
     const int t = threadIdx.x;
-    const uint16_t* xp = x + (size_t)blockIdx.x * N;
+    const typename Elem<DT>::type* xp = x + (size_t)blockIdx.x * N;
     const uint32_t mc = (uint32_t)st[blockIdx.x].med_code;
     int r = st[blockIdx.x].med_r;
     if (t == 0) found = -1;
@@ -274,7 +284,7 @@ __device__ void heap_sort_serial(unsigned long long* A, long long f, long long l
 }
 
 template <int DT>
-__global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restrict__ x, long long N,
+__global__ void __launch_bounds__(NT) k_plane_mode_idx(const typename Elem<DT>::type* __restrict__ x, long long N,
                                                       const PlaneStat* __restrict__ st, unsigned long long* ws,
                                                       int64_t* __restrict__ idx, int depth_limit) {
     __shared__ int sh[2 * NW];
@@ -282,7 +292,7 @@ __global__ void __launch_bounds__(NT) k_plane_mode_idx(const uint16_t* __restric
     __shared__ unsigned long long sh_e[4];
     __shared__ unsigned long long sh_u[2];
     const int t = threadIdx.x;
-    const uint16_t* xp = x + (size_t)blockIdx.x * N;
+    const typename Elem<DT>::type* xp = x + (size_t)blockIdx.x * N;
     const PlaneStat s = st[blockIdx.x];
     const uint32_t m = (uint32_t)s.mode_code;
     // per plane: the working array and the swap slots (L then R) as u64 [N] each, ranks int2 [N]
@@ -491,6 +501,36 @@ int admm_planestat_median_mode(int dtype, const void* x, int64_t P, int64_t N, i
         if (mode_idx)
             hipLaunchKernelGGL(k_plane_mode_idx<ADMM_CHANSTAT_F16>, grid, block, 0, s, xp, (long long)N, st, buf,
                                mode_idx, depth_limit);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : ADMM_TV_EHIP;
+}
+
+int admm_planestat_select(int dtype, const void* x, int64_t P, int64_t N, const int32_t* stats, int64_t* median_idx,
+                          int64_t* mode_idx, void* ws, size_t ws_bytes, int depth_limit, void* stream) {
+    if (!x || !stats || P < 0 || N < 1 || depth_limit > 62) return ADMM_TV_EINVAL;
+    if (N > (1LL << 31) - 2) return ADMM_TV_EUNSUPPORTED;
+    if (P == 0) return 0;
+    size_t need = 0;
+    admm_planestat_workspace_size(P, N, &need);
+    if (mode_idx && (!ws || ws_bytes < need)) return ADMM_TV_EWORKSPACE;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const PlaneStat* st = reinterpret_cast<const PlaneStat*>(stats);
+    auto* buf = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) +
+                                                      ((P * sizeof(PlaneStat) + 255) / 256) * 256);
+    const dim3 grid((unsigned)P), block(NT);
+    auto run = [&](auto dt) {
+        constexpr int DT = decltype(dt)::value;
+        using E = typename Elem<DT>::type;
+        const E* xp = static_cast<const E*>(x);
+        if (median_idx) hipLaunchKernelGGL(k_plane_median_idx<DT>, grid, block, 0, s, xp, (long long)N, st, median_idx);
+        if (mode_idx)
+            hipLaunchKernelGGL(k_plane_mode_idx<DT>, grid, block, 0, s, xp, (long long)N, st, buf, mode_idx, depth_limit);
+    };
+    switch (dtype) {
+        case ADMM_CHANSTAT_F32: run(std::integral_constant<int, ADMM_CHANSTAT_F32>{}); break;
+        case ADMM_CHANSTAT_BF16: run(std::integral_constant<int, ADMM_CHANSTAT_BF16>{}); break;
+        case ADMM_CHANSTAT_F16: run(std::integral_constant<int, ADMM_CHANSTAT_F16>{}); break;
+        default: return ADMM_TV_EINVAL;
     }
     return hipGetLastError() == hipSuccess ? 0 : ADMM_TV_EHIP;
 }
