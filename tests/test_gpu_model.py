@@ -2,10 +2,13 @@
 ADMM modules on the HIP solver, against the reference's own model run in fp64
 (tests/golden/g8_model_admm.npz: reduced width, reference weights loaded by state_dict).
 
-The model's channel statistics include torch.mode over whole planes: in fp32 two pixels of a
-plane can round to the same value and the mode jumps to that pair (measured: one of 48 planes
-on the GPU, moving the output by 1.4e-3), so an end-to-end fp32 GPU run is not comparable with
-an fp64 run at solver precision.  The parity test therefore splits at the solver:
+The model's channel statistics include median / mode over channels and over whole planes.  The
+HIP statistics kernels follow the reference's CPU tie rules, and an end-to-end fp32 GPU run can
+match the reference's fp64 model to ~5e-8; but two nearly equal fp32 values can become equal (or
+swap) under a different rounding of an upstream convolution (MIOpen's algorithm choice, atomic
+accumulation order), and the selected element then jumps (measured on the same box: 5.2e-8 in
+one process, 3.1e-3 in another).  An end-to-end fp32 run is therefore not comparable with an
+fp64 run at solver precision, and the parity test splits at the solver:
 
 * forward: the ADMM modules run on the GPU inside the model; the CNN downstream of them is
   re-run in fp64 (CPU) on their outputs -> must reproduce the reference's fp64 output (1e-6);
@@ -14,7 +17,7 @@ an fp64 run at solver precision.  The parity test therefore splits at the solver
   autograd (1e-5 / 1e-4, the (lambda, rho) pair of a module compared as one vector: the rho
   gradient alone can be a ~1e-6 cancellation residue next to a lambda gradient of ~1).
 
-The end-to-end GPU run (MIOpen convs, torch.mode on the GPU) is reported and gated loosely.
+The end-to-end GPU run (MIOpen convs, the HIP solver and statistics) is reported and gated loosely.
 """
 import numpy as np
 import pytest
@@ -106,7 +109,7 @@ def test_model_forward_backward_end_to_end(cuda_dev):
             errs[k] = rel(v, ref)
     worst = max(errs, key=errs.get)
     print(f"out {e_out:.2e}  x.grad {e_gx:.2e}  worst param grad {worst} {errs[worst]:.2e}")
-    # loose: torch.mode over fp32 planes (see module docstring) -- a whole-model sanity bound
+    # loose: fp32 near-ties in the statistics (see module docstring) -- a whole-model sanity bound
     assert e_out <= 1e-2
     assert e_gx <= 1e-1
 
