@@ -99,8 +99,7 @@ __device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restr
 //  2. outputs k and R - k take conjugate twiddles W_R^{+-qk}: an item computes GP such output
 //     pairs of one butterfly (group 0 also output 0), reading each input once and each table
 //     twiddle once for both outputs of a pair -- (1 + GP) LDS reads per input for 2 GP outputs
-//     instead of 2 per input per output, and the two complex products share their four real
-//     multiplies.
+//     instead of 2 per input per output, and the two complex products are eight FMAs.
 #ifndef ADMM_GP
 #define ADMM_GP 2
 #endif
@@ -140,7 +139,8 @@ __device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict_
         cf x0 = col[0];
         cf acc0 = x0;  // output 0 (group 0 only)
         cf ap[GP], am[GP];
-        int idx[GP];
+        int idx[GP];  // table index (q (k0 + j) mod R) * rstep, stepped without multiply or modulo
+        const int wrap = R * rstep;
 #pragma unroll
         for (int j = 0; j < GP; ++j) {
             ap[j] = x0;
@@ -153,12 +153,14 @@ __device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict_
             acc0 = cadd(acc0, x);
 #pragma unroll
             for (int j = 0; j < GP; ++j) {
-                idx[j] += k0 + j;
-                if (idx[j] >= R) idx[j] -= R;
-                const cf w = twid<DIR>(tw, idx[j] * rstep);
-                const float rr = x.x * w.x, ii = x.y * w.y, ri = x.x * w.y, ir = x.y * w.x;
-                ap[j] = mkc(ap[j].x + (rr - ii), ap[j].y + (ri + ir));  // x w
-                am[j] = mkc(am[j].x + (rr + ii), am[j].y + (ir - ri));  // x conj(w)
+                idx[j] += (k0 + j) * rstep;
+                if (idx[j] >= wrap) idx[j] -= wrap;
+                const cf w = twid<DIR>(tw, idx[j]);
+                // x w and x conj(w) accumulated with eight FMAs
+                ap[j].x = fmaf(-x.y, w.y, fmaf(x.x, w.x, ap[j].x));
+                ap[j].y = fmaf(x.y, w.x, fmaf(x.x, w.y, ap[j].y));
+                am[j].x = fmaf(x.y, w.y, fmaf(x.x, w.x, am[j].x));
+                am[j].y = fmaf(-x.x, w.y, fmaf(x.y, w.x, am[j].y));
             }
         }
         cf* out = dst + ((size_t)(vt / NS) * span + m) * lines + c;
