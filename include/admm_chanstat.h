@@ -69,9 +69,11 @@ int admm_chanstat_pool_backward(int dtype, const void* x, const void* out, const
                                 int64_t B, int64_t C, int64_t HW, void* gx, void* stream);
 
 /* ---- whole-plane median and mode (ChannelWiseAttention's amedian / amodes, reference
- * elayers/cwa.py: x.view(B, C, -1).median(-1) / .mode(-1)), 16-bit types only.
- * x          : [P][N] elements of `dtype` (ADMM_CHANSTAT_BF16 or _F16)
- * median_idx : [P] int64, flat index of torch.median's (CPU) element, or NULL
+ * elayers/cwa.py: x.view(B, C, -1).median(-1) / .mode(-1)).
+ * x          : [P][N] elements of `dtype` (ADMM_CHANSTAT_BF16 or _F16; ADMM_CHANSTAT_F32 for
+ *              the median only: mode_idx must then be NULL, else ADMM_TV_EUNSUPPORTED)
+ * median_idx : [P] int64, flat index of torch.median's (CPU) element, or NULL; a plane holding
+ *              NaN gives its first NaN, as torch.median does
  * mode_idx   : [P] int64, flat index of torch.mode's (CPU) element, or NULL
  * ws         : device workspace of admm_planestat_workspace_size(P, N) bytes (24 N B per plane)
  * depth_limit: -1 (std::sort's 2*floor(log2 N)); >= 0 forces the introsort depth budget (tests)

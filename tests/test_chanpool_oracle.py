@@ -134,9 +134,11 @@ def test_chanstat_header_binding_and_exports():
     n = ctypes.c_size_t(0)
     assert lib.admm_planestat_workspace_size(1376, 512 * 512, ctypes.byref(n)) == 0
     assert n.value >= 1376 * 24 * 512 * 512
-    # plane statistics: fp32 unsupported (16-bit codes only), workspace checked before any launch
-    assert lib.admm_planestat_median_mode(_native.CHANSTAT_F32, 8, 2, 16, None, None, 8, 1 << 20, -1, None) \
+    # plane statistics: fp32 takes the median only, workspace checked before any launch
+    assert lib.admm_planestat_median_mode(_native.CHANSTAT_F32, 8, 2, 16, None, 8, 8, 1 << 20, -1, None) \
         == _native.ADMM_TV_EUNSUPPORTED
+    assert lib.admm_planestat_median_mode(_native.CHANSTAT_F32, 8, 2, 16, 8, None, 8, 16, -1, None) \
+        == _native.ADMM_TV_EWORKSPACE
     assert lib.admm_planestat_median_mode(_native.CHANSTAT_BF16, 8, 2, 16, None, None, 8, 16, -1, None) \
         == _native.ADMM_TV_EWORKSPACE
     assert lib.admm_planestat_median_mode(_native.CHANSTAT_BF16, 8, 0, 16, None, None, None, 0, -1, None) == 0

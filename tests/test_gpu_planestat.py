@@ -36,6 +36,38 @@ def test_median_mode_vs_torch_cpu(cuda_dev, dt, shape):
         assert torch.equal(flat.gather(1, oi[:, None]).squeeze(1), mod.values)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+def test_median_nan_signed_zero_inf(cuda_dev, dt):
+    # torch.median's CPU rules: a plane holding NaN gives its first NaN; -0 and +0 tie (flat
+    # order decides); infinities order as numbers
+    from admmtor.elayers.cwa import plane_select_native
+    g = torch.Generator().manual_seed(21)
+    x = (torch.randint(-3, 4, (4, 1, 16, 33), generator=g).double() / 2).to(dt)
+    x[0, 0, 3, 5] = float("nan")
+    x[0, 0, 9, 1] = float("nan")
+    x[1, 0, 0, :8] = -0.0
+    x[1, 0, 2, :8] = float("inf")
+    x[2, 0, 1, :30] = float("-inf")
+    x[3].fill_(-0.0)
+    x[3, 0, ::2, ::3] = 0.0
+    flat = x.reshape(4, -1)
+    mi = plane_select_native(x.to(cuda_dev), "median").cpu()
+    assert torch.equal(mi, flat.median(dim=1).indices)
+
+
+def test_fp32_median_low_bits(cuda_dev):
+    # codes that share their high 16 bits and differ only in the low ones (the radix select's
+    # second pass), with ties, at a 512x512 plane size
+    from admmtor.elayers.cwa import plane_select_native
+    g = torch.Generator().manual_seed(22)
+    k = torch.randint(0, 40, (3, 2, 512, 512), generator=g).double()
+    x = (1.0 + k * 2.0 ** -20).float()
+    x[1] = -x[1]
+    flat = x.reshape(6, -1)
+    mi = plane_select_native(x.to(cuda_dev), "median").cpu()
+    assert torch.equal(mi, flat.median(dim=1).indices)
+
+
 def test_unique_values_and_small_planes(cuda_dev):
     from admmtor.elayers.cwa import plane_select_native
     x = torch.randperm(10, generator=torch.Generator().manual_seed(1)).to(torch.bfloat16).reshape(1, 1, 2, 5)

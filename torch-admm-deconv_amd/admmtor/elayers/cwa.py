@@ -33,30 +33,25 @@ def _ord32(v: torch.Tensor) -> torch.Tensor:
     return torch.where(mag > 0x7F800000, torch.full_like(o, 0xFFFFFFFF), o)
 
 
-def _plane_stats_f32(flat: torch.Tensor, which: str) -> torch.Tensor:
-    """(P, N) fp32 -> (P, 4) int32 {mode code, mode count, median code, median rank in its run}
-    (the 16-bit types get these from the kernels' LDS histogram).  median: the value from
-    torch's median, its rank from a count of smaller values; mode: runs of one segmented sort."""
+def _plane_mode_stats_f32(flat: torch.Tensor) -> torch.Tensor:
+    """(P, N) fp32 -> (P, 4) int32 {mode code, mode count, 0, 0} from the runs of one segmented
+    sort (the 16-bit types get these from the kernels' LDS histogram, the fp32 median from a
+    radix select in the library)."""
     P, N = flat.shape
     st = torch.zeros((P, 4), dtype=torch.int64, device=flat.device)
-    if which == "median":
-        vm = flat.median(dim=1).values
-        st[:, 2] = _ord32(vm)
-        st[:, 3] = (N - 1) // 2 - (flat < vm[:, None]).sum(dim=1)
-    else:
-        sv = torch.sort(flat, dim=1).values
-        start = torch.ones((P, N), dtype=torch.bool, device=flat.device)
-        start[:, 1:] = sv[:, 1:] != sv[:, :-1]
-        pos = torch.arange(N, device=flat.device, dtype=torch.int32).expand(P, N)
-        # next run start after each position (N past the last), by a reversed running minimum
-        nxt = torch.full((P, N), N, device=flat.device, dtype=torch.int32)
-        nxt[:, :-1] = torch.where(start[:, 1:], pos[:, 1:], nxt[:, 1:])
-        nxt = torch.flip(torch.cummin(torch.flip(nxt, [1]), dim=1).values, [1])
-        length = torch.where(start, nxt - pos, torch.zeros_like(pos))
-        mcount = length.max(dim=1).values
-        first = torch.argmax((length == mcount[:, None]).to(torch.int8), dim=1)  # first longest run
-        st[:, 0] = _ord32(sv.gather(1, first[:, None]).squeeze(1))
-        st[:, 1] = mcount.to(torch.int64)
+    sv = torch.sort(flat, dim=1).values
+    start = torch.ones((P, N), dtype=torch.bool, device=flat.device)
+    start[:, 1:] = sv[:, 1:] != sv[:, :-1]
+    pos = torch.arange(N, device=flat.device, dtype=torch.int32).expand(P, N)
+    # next run start after each position (N past the last), by a reversed running minimum
+    nxt = torch.full((P, N), N, device=flat.device, dtype=torch.int32)
+    nxt[:, :-1] = torch.where(start[:, 1:], pos[:, 1:], nxt[:, 1:])
+    nxt = torch.flip(torch.cummin(torch.flip(nxt, [1]), dim=1).values, [1])
+    length = torch.where(start, nxt - pos, torch.zeros_like(pos))
+    mcount = length.max(dim=1).values
+    first = torch.argmax((length == mcount[:, None]).to(torch.int8), dim=1)  # first longest run
+    st[:, 0] = _ord32(sv.gather(1, first[:, None]).squeeze(1))
+    st[:, 1] = mcount.to(torch.int64)
     st = torch.where(st >= 2 ** 31, st - 2 ** 32, st)  # 32-bit codes as int32 bit patterns
     return st.to(torch.int32).contiguous()
 
@@ -84,11 +79,10 @@ def plane_select_native(x: torch.Tensor, which: str, depth_limit=None) -> torch.
         n = min(chunk, P - p0)
         out = idx[p0:p0 + n].data_ptr()
         dl = -1 if depth_limit is None else int(depth_limit)
-        if x.dtype == torch.float32:
-            st = _plane_stats_f32(flat[p0:p0 + n], which)
+        if x.dtype == torch.float32 and which == "mode":
+            st = _plane_mode_stats_f32(flat[p0:p0 + n])
             _native.check(lib.admm_planestat_select(
-                0, flat[p0].data_ptr(), n, N, st.data_ptr(), out if which == "median" else None,
-                out if which == "mode" else None, ws.data_ptr(), ws.numel(), dl, stream))
+                0, flat[p0].data_ptr(), n, N, st.data_ptr(), None, out, ws.data_ptr(), ws.numel(), dl, stream))
         else:
             _native.check(lib.admm_planestat_median_mode(
                 _PLANE_DTYPES[x.dtype], flat[p0].data_ptr(), n, N, out if which == "median" else None,

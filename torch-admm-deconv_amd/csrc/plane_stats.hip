@@ -114,6 +114,7 @@ __global__ void __launch_bounds__(NT) k_plane_hist(const uint16_t* __restrict__ 
     uint32_t* hist = reinterpret_cast<uint32_t*>(smem);  // [32768]
     __shared__ int sh_i[2 * NW];
     __shared__ unsigned long long sh_best;
+    __shared__ int sh_nan;
     const int t = threadIdx.x;
     const uint16_t* xp = x + (size_t)blockIdx.x * N;
     const long long mpos = (N - 1) >> 1;
@@ -169,6 +170,7 @@ __global__ void __launch_bounds__(NT) k_plane_hist(const uint16_t* __restrict__ 
             __syncthreads();
             rs = off + (int)v - (int)sum;  // exclusive
         }
+        if (half == 1 && t == NT - 1) sh_nan = (int)hist[0x7FFF];  // code 0xFFFF: NaN
         const long long lo = below + rs, hi = lo + sum;
         if (med_code < 0 && mpos >= lo && mpos < hi) {  // exactly one thread of the block
             long long acc = lo;
@@ -198,7 +200,106 @@ __global__ void __launch_bounds__(NT) k_plane_hist(const uint16_t* __restrict__ 
         if (t == 0) sh_best = 0;
         __syncthreads();
     }
+    if (sh_nan > 0) {  // torch.median: a plane holding NaN gives its first NaN
+        med_code = 0xFFFF;
+        med_r = 0;
+    }
     if (t == 0) st[blockIdx.x] = PlaneStat{best_code, best_count, med_code, med_r};
+}
+
+// ---------------------------------------------------------------- fp32 median (radix select)
+// Rank `target` among the 16-bit keys (c >> shift) & 0xFFFF of the codes c of a plane (only
+// codes whose high half equals `hi` when `filter`): LDS histogram, half the key space per
+// pass, the second half skipped once the target is found.  Returns the key and the target's
+// rank among the elements with that key.
+__device__ void hist_rank16(const uint32_t* __restrict__ xp, long long N, int shift, bool filter, uint32_t hi,
+                            long long target, uint32_t* hist, int* sh_i, int* sh_nan, int& key, int& rank) {
+    const int t = threadIdx.x;
+    long long below = 0;
+    for (int half = 0; half < 2; ++half) {
+        for (int i = t; i < 32768; i += NT) hist[i] = 0u;
+        __syncthreads();
+        bool nan = false;
+#pragma unroll 8
+        for (long long i = t; i < N; i += NT) {
+            const uint32_t c = ord32_f32(xp[i]);
+            const uint32_t k = (c >> shift) & 0xFFFFu;
+            nan |= c == 0xFFFFFFFFu;
+            if ((!filter || (c >> 16) == hi) && (int)(k >> 15) == half) atomicAdd(&hist[k & 0x7FFFu], 1u);
+        }
+        if (nan) *sh_nan = 1;
+        __syncthreads();
+        const int b0 = t * 32;
+        uint32_t sum = 0;
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) sum += hist[b0 + i];
+        uint32_t v = sum;
+        const int lane = t & 63, w = t >> 6;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)v, o);
+            if (lane >= o) v += u;
+        }
+        if (lane == 63) sh_i[w] = (int)v;
+        __syncthreads();
+        long long off = 0, tot = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            if (i < w) off += sh_i[i];
+            tot += sh_i[i];
+        }
+        __syncthreads();
+        const long long lo = below + off + (long long)v - sum;
+        if (target >= lo && target < lo + sum) {  // exactly one thread of the block
+            long long acc = lo;
+            for (int i = 0; i < 32; ++i) {
+                const uint32_t h = hist[b0 + i];
+                if (target < acc + h) {
+                    sh_i[0] = (half << 15) | (b0 + i);
+                    sh_i[1] = (int)(target - acc);
+                    break;
+                }
+                acc += h;
+            }
+        }
+        __syncthreads();
+        if (target < below + tot) {  // uniform
+            key = sh_i[0];
+            rank = sh_i[1];
+            __syncthreads();
+            return;
+        }
+        below += tot;
+    }
+    key = 0xFFFF;  // not reached: target < N
+    rank = 0;
+}
+
+// {median code, rank in its run} of each fp32 plane: the high 16 bits of the median's code by
+// one histogram pass, the low 16 bits by a second over the elements of that high key
+__global__ void __launch_bounds__(NT) k_plane_median32(const uint32_t* __restrict__ x, long long N,
+                                                      PlaneStat* __restrict__ st) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint32_t* hist = reinterpret_cast<uint32_t*>(smem);  // [32768]
+    __shared__ int sh_i[2 * NW];
+    __shared__ int sh_nan;
+    const int t = threadIdx.x;
+    const uint32_t* xp = x + (size_t)blockIdx.x * N;
+    if (t == 0) sh_nan = 0;
+    __syncthreads();
+    const long long mpos = (N - 1) >> 1;
+    int khi, rhi, klo = 0, rlo = 0;
+    hist_rank16(xp, N, 16, false, 0u, mpos, hist, sh_i, &sh_nan, khi, rhi);
+    int code, r;
+    if (sh_nan) {  // torch.median: a plane holding NaN gives its first NaN (uniform branch)
+        code = (int)0xFFFFFFFFu;
+        r = 0;
+    } else {
+        hist_rank16(xp, N, 0, true, (uint32_t)khi, rhi, hist, sh_i, &sh_nan, klo, rlo);
+        code = (int)(((uint32_t)khi << 16) | (uint32_t)klo);
+        r = rlo;
+    }
+    if (t == 0) st[blockIdx.x] = PlaneStat{0, 0, code, r};
 }
 
 // --------------------------------------------------------------------------- median index
@@ -466,7 +567,8 @@ int admm_planestat_workspace_size(int64_t P, int64_t N, size_t* bytes) {
 int admm_planestat_median_mode(int dtype, const void* x, int64_t P, int64_t N, int64_t* median_idx,
                                int64_t* mode_idx, void* ws, size_t ws_bytes, int depth_limit, void* stream) {
     if (!x || P < 0 || N < 1 || depth_limit > 62) return ADMM_TV_EINVAL;
-    if (dtype != ADMM_CHANSTAT_BF16 && dtype != ADMM_CHANSTAT_F16) return ADMM_TV_EUNSUPPORTED;
+    if (dtype != ADMM_CHANSTAT_BF16 && dtype != ADMM_CHANSTAT_F16 && !(dtype == ADMM_CHANSTAT_F32 && !mode_idx))
+        return ADMM_TV_EUNSUPPORTED;
     if (N > (1LL << 31) - 2) return ADMM_TV_EUNSUPPORTED;
     if (P == 0) return 0;
     size_t need = 0;
@@ -474,6 +576,18 @@ int admm_planestat_median_mode(int dtype, const void* x, int64_t P, int64_t N, i
     if (!ws || ws_bytes < need) return ADMM_TV_EWORKSPACE;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     PlaneStat* st = reinterpret_cast<PlaneStat*>(ws);
+    if (dtype == ADMM_CHANSTAT_F32) {  // median only (radix select over the 32-bit codes)
+        if (!median_idx) return 0;
+        const size_t lds = 32768 * sizeof(uint32_t);
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_plane_median32),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return ADMM_TV_EHIP;
+        const uint32_t* xp = static_cast<const uint32_t*>(x);
+        hipLaunchKernelGGL(k_plane_median32, dim3((unsigned)P), dim3(NT), lds, s, xp, (long long)N, st);
+        hipLaunchKernelGGL(k_plane_median_idx<ADMM_CHANSTAT_F32>, dim3((unsigned)P), dim3(NT), 0, s, xp, (long long)N,
+                           st, median_idx);
+        return hipGetLastError() == hipSuccess ? 0 : ADMM_TV_EHIP;
+    }
     auto* buf = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) +
                                                       ((P * sizeof(PlaneStat) + 255) / 256) * 256);
     const uint16_t* xp = static_cast<const uint16_t*>(x);
