@@ -28,7 +28,9 @@ Pinning: ``tests/test_chanpool_oracle.py`` checks this restatement against torch
 committed fixture ``tests/golden/g9_chanpool.npz`` (written by ``tests/golden/make_golden_chanpool.py``
 from torch's CPU kernels); the heapsort fallback (reached only through the depth budget) is
 checked against ``std::make_heap`` + ``std::sort_heap`` compiled here with g++.
-NaN inputs are unpinned: ``<`` is not a strict weak order with NaN.
+NaN inputs: the mode is unpinned (``<`` is not a strict weak order with NaN); the median of a
+column holding NaN is its first NaN (torch.median's rule), which the GPU tests check against
+torch's CPU kernels directly.
 """
 from __future__ import annotations
 

@@ -63,6 +63,21 @@ def test_vs_torch_cpu(cuda_dev, dt, C):
             assert torch.isnan(out[:, 0]).all()
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+def test_median_nan_rule(cuda_dev, dt):
+    # torch.median: a column holding NaN gives its first NaN (value and channel)
+    gen = torch.Generator().manual_seed(31)
+    x = (torch.randint(-3, 4, (2, 86, 4, 9), generator=gen).double() / 2).to(dt)
+    x[0, 5, 0, 0] = x[0, 40, 0, 0] = float("nan")
+    x[0, 80, 1, 2] = float("nan")
+    x[1, 0, 3, 8] = float("nan")
+    x[1, :, 2, 2] = float("nan")
+    out, idx = _run(x.to(cuda_dev))
+    med = x.median(dim=1)
+    assert torch.equal(idx[:, 0], med.indices)
+    assert torch.equal(out[:, 1].isnan(), med.values.isnan())
+
+
 @pytest.mark.parametrize("depth", [0, 1, 3])
 def test_depth_limited_sort_vs_oracle(cuda_dev, depth):
     # the heapsort fallback is reached only through the depth budget: force it and compare with

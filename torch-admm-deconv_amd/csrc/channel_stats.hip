@@ -406,8 +406,16 @@ __global__ void __launch_bounds__(256) k_chanpool(const typename T::store* __res
         }
         wave_bitonic(key, lane);
 
-        // median: sorted position mpos of the (value, channel) order
-        const int mi = (int)(rd_key(key, mpos) & 0xFF);
+        // median: sorted position mpos of the (value, channel) order; a column holding NaN gives
+        // its first NaN (torch.median)
+        constexpr uint32_t kNaN = T::bits == 32 ? 0xFFFFFFFFu : ((1u << T::bits) - 1u);
+        int mi = -1;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint64_t nb = __ballot(valid[e] && val[e] == kNaN);
+            if (mi < 0 && nb) mi = e * 64 + __builtin_ctzll(nb);
+        }
+        if (mi < 0) mi = (int)(rd_key(key, mpos) & 0xFF);
 
         // runs of equal values in the sorted keys: starts, lengths, the first longest run
         uint32_t sv[E];
