@@ -480,7 +480,14 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
     load_tw(tw, a.twW, W);
     __syncthreads();
     const int sgl = threadIdx.x / L, t = threadIdx.x % L;
-    const long long strip = (long long)blockIdx.x * G::SG + sgl;
+    // XCD remap of the strips (-DADMM_PASSA_REMAP=0/1 for A/B runs; default: W <= 512): C2
+    // pass A +2 %, C3 -7 % (interleaved A/B, tools/ab_variants.sh)
+#ifndef ADMM_PASSA_REMAP
+#define ADMM_PASSA_REMAP -1
+#endif
+    constexpr bool kRemap = ADMM_PASSA_REMAP < 0 ? N <= 256 : ADMM_PASSA_REMAP != 0;
+    const unsigned blk = kRemap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const long long strip = (long long)blk * G::SG + sgl;
     if (strip >= a.nstrips) return;
     const int H = a.H, R = a.R;
     const int spp = H / R;
