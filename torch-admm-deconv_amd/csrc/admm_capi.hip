@@ -414,15 +414,21 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
     return 0;
 }
 
-int strip_rows(int H, int N, long long rows) {
+int strip_rows(int H, int N, long long rows, bool aniso_fwd = false) {
     int R = env_int("ADMM_PASSA_R", 0);
     if (R <= 0) {
-        // rows per strip (measured on MI355X, tools/sweep.py: R = 8 beats 16 at W = 512 and
-        // 1024 with the 3-waves/SIMD row pass); halve while there are fewer than ~3 waves per
-        // SIMD of strips
+        // rows per strip (measured on MI355X, tools/sweep.py: R = 8 beats 16 at W = 1024 with
+        // the 3-waves/SIMD row pass); halve while there are fewer than ~3 waves per SIMD of
+        // strips.  The aniso forward at W = 512 (with the XCD strip remap) takes R = 16 down to
+        // ~1.5 waves per SIMD of strips: C2 pass A 0.126 -> 0.120 ms; the iso row pass there
+        // keeps the rule (C5 module: R = 4 best).
         const int L = std::min(64, N / (N >= 1024 ? 16 : N >= 64 ? 8 : N >= 16 ? 4 : 2));
-        const long long want = 3LL * 1024 * 64 / L;
+        long long want = 3LL * 1024 * 64 / L;
         R = 8;
+        if (aniso_fwd && N == 256) {
+            R = 16;
+            want /= 2;
+        }
         while (R > 2 && rows / R < want) R /= 2;
     }
     if (R > H) R = H;
@@ -741,7 +747,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, t0, twW, Pm * H, s); });
         if (e) return e;
     }
-    const int R = strip_rows(H, N, rows);
+    const int R = strip_rows(H, N, rows, !d.iso && !hist);
 
     int cur = 0, uin = 0;  // spec[cur] holds the current r spectra; u[2*uin], u[2*uin+1] = u_x, u_y in
     for (int it = 1; it <= d.maxit; ++it) {
