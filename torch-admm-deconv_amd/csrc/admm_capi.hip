@@ -136,15 +136,16 @@ Layout make_layout(const admm_tv_desc& d) {
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
         // plane groups for the iso norm pass: enough (group,row) items to fill the chip
-        // planes per group: at most 16 (each group writes and the reduce reads one 2HW partial;
-        // C3 iso: 16 -> 507 it/s, 8 -> 499),
+        // planes per group: at most 64 (each group writes and the reduce reads one 2HW partial;
+        // C3 iso norm pass: 16 -> 0.49 ms, 32 -> 0.46, 64 -> 0.45; 8 -> 499 it/s, 16 -> 497-507,
+        // 64 -> 509),
         // fewer when (group, row) items would not give ~3 waves per SIMD (C5: 48 planes of 512^2
         // -> 4, iso norm -30 %)
         const int lanes = (int)std::min<size_t>(64, N / (N >= 1024 ? 16 : N >= 64 ? 8 : N >= 16 ? 4 : 2));
         const long long want = 3LL * 1024 * 64 / std::max(lanes, 1);
-        int ppg = (int)std::max<long long>(1, std::min<long long>(16, (long long)(P * H) / want));
-        ppg = env_int("ADMM_ISO_PPG", ppg);
-        if ((size_t)P <= (size_t)ppg) ppg = (int)P;
+        int ppg = (int)std::max<long long>(1, std::min<long long>(64, (long long)(P * H) / want));
+        if (const int e = env_int("ADMM_ISO_PPG", 0); e > 0) ppg = e;  // A/B knob; <= 0: the rule
+        if ((size_t)P <= (size_t)ppg) ppg = (int)std::max<long long>(1, P);
         if (G > 1) {  // a plane group must not straddle two modules: a divisor of B*C
             const int pm = (int)(d.B * d.C);
             ppg = std::min(ppg, pm);
@@ -490,10 +491,15 @@ GPlan make_plan(int n) {
 int pow2_floor(int v) { int p = 1; while (2 * p <= v) p *= 2; return p; }
 // LDS image <= ~32 KB (4+ resident blocks per CU: the prime-radix stages are latency-bound
 // chains and need the waves), except where one line alone is bigger
+// (A/B knobs ADMM_GROW_LINES / ADMM_GCOL_COLS: rounded down to a power of two in [1, 32])
 int grow_lines(int W) {
-    return env_int("ADMM_GROW_LINES", pow2_floor(std::max(1, std::min(32, (4096 / W - 1) / 2))));
+    const int dflt = pow2_floor(std::max(1, std::min(32, (4096 / W - 1) / 2)));
+    return pow2_floor(std::max(1, std::min(32, env_int("ADMM_GROW_LINES", dflt))));
 }
-int gcol_cols(int H) { return env_int("ADMM_GCOL_COLS", pow2_floor(std::max(1, std::min(16, (4096 / H - 1) / 2)))); }
+int gcol_cols(int H) {
+    const int dflt = pow2_floor(std::max(1, std::min(16, (4096 / H - 1) / 2)));
+    return pow2_floor(std::max(1, std::min(32, env_int("ADMM_GCOL_COLS", dflt))));
+}
 
 int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hipStream_t s) {
     GRowArgs a{img, spec, nullptr, tw, make_plan(W), rows, grow_lines(W)};
