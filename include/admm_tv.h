@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ADMM_TV_ABI_VERSION 3
+#define ADMM_TV_ABI_VERSION 4
 
 enum {
     ADMM_TV_OK = 0,
@@ -42,6 +42,15 @@ enum {
     ADMM_TV_EHIP = -5,          /* a HIP runtime call or kernel launch failed       */
     ADMM_TV_EKERNEL = -6        /* PSF larger than the image                        */
 };
+
+/* Cross-rank reduction for iso (block) shrinkage over a batch sharded across GPUs
+ * (SURVEY.md §8 e2).  The per-pixel norm couples every (b,c) plane, so each iteration the
+ * library calls allreduce(buf, count, stream, allreduce_ctx) on its per-pixel sums
+ * (count = groups*2*H*W floats, device memory inside the caller's workspace or history
+ * buffer) and expects an in-place SUM all-reduce ordered on `stream` (e.g. RCCL).  The
+ * backward calls it the same way on the cross-plane products Q.  The callback runs on the
+ * calling thread, inside the admm_tv_forward* / admm_tv_backward call that was given it. */
+typedef void (*admm_tv_allreduce_fn)(float* buf, size_t count, void* stream, void* ctx);
 
 /* Problem descriptor.  Replaces the shapes/flags of fft_admm_tv's arguments
  * (deconv.py:35-42): xin (B,C,H,W), kern (1,1,kh,kw) or empty (kh = kw = 0),
@@ -54,7 +63,13 @@ enum {
  * sequence -- the two ADMMDeconv modules of DivergentAttention's first level
  * (blocks.py:187-196).  out / gout / history then hold G*B*C planes (module-major),
  * glam / grho G values, gxin the sum over modules.  Each module's iso norm runs over its
- * own (B,C).  Fused power-of-two sizes only, no PSF gradient. */
+ * own (B,C).  Fused power-of-two sizes only, no PSF gradient.
+ *
+ * allreduce / allreduce_ctx: the per-call cross-rank hook above (NULL: single process;
+ * ignored for iso = 0).  Everything a call needs is in its arguments: the library keeps no
+ * per-solve global state, so calls on different threads / streams are independent.
+ * With a hook, B*C may be 0 (a rank whose shard is empty): the call then only takes part
+ * in the reductions (zeros), so the other ranks' collectives complete. */
 typedef struct admm_tv_desc {
     int64_t B, C, H, W;
     int32_t kh, kw;
@@ -62,6 +77,8 @@ typedef struct admm_tv_desc {
     int32_t maxit;
     int32_t flags;   /* ADMM_TV_FLAG_*; 0 for plain use */
     int32_t groups;  /* modules solved together (0 or 1: one) */
+    admm_tv_allreduce_fn allreduce;  /* iso over a sharded batch; NULL otherwise */
+    void* allreduce_ctx;
 } admm_tv_desc;
 
 /* flags: the training forward also keeps the spectra of every r_k so that
@@ -70,6 +87,10 @@ typedef struct admm_tv_desc {
 
 /* ABI version (ADMM_TV_ABI_VERSION). */
 int admm_tv_abi_version(void);
+
+/* Provenance: the first 16 hex digits of the SHA-256 of the sources the library was built
+ * from (the .hip / .hpp files of csrc, the .h files of include, csrc/Makefile). */
+const char* admm_tv_build_hash(void);
 
 /* 1: (H, W) runs on the fused power-of-two kernels (H in [16,4096], W in [16,2048]);
  * 2: any other size in [1,4096] x [1,4096], run on the generic kernels (mixed-radix
@@ -119,18 +140,9 @@ int admm_tv_backward(const admm_tv_desc* desc, const float* xin, const float* ke
 int admm_tv_psf_transpose(const admm_tv_desc* desc, const float* xin, const float* kern,
                           float* out, void* workspace, size_t workspace_bytes, void* stream);
 
-/* Cross-rank reduction hook for iso (block) shrinkage over a batch sharded across
- * GPUs.  The per-pixel norm couples every (b,c) plane, so each
- * iteration the library calls fn(buf, count, stream, ctx) on its per-pixel sums
- * (count = 2*H*W floats, device memory inside the workspace or history buffer)
- * and expects an in-place SUM all-reduce ordered on `stream` (e.g. RCCL).  In the
- * backward the same is called on the cross-plane products Q.  NULL disables
- * (single process).  Global to the process; not used for iso = 0.               */
-typedef void (*admm_tv_allreduce_fn)(float* buf, size_t count, void* stream, void* ctx);
-int admm_tv_set_allreduce(admm_tv_allreduce_fn fn, void* ctx);
-
 /* Per-kernel timing of the iteration passes (HIP events on the launch stream),
- * used by bench.py for the roofline line.  enable != 0 starts recording;
+ * used by bench.py for the roofline line (process-wide, behind a lock: calls from several
+ * threads add to the same totals).  enable != 0 starts recording;
  * read() synchronises on the recorded events and returns totals since the last
  * reset: ms[k], count[k] for k = 0 pass A (row pass), 1 pass B (column pass),
  * 2 iso norm pass, 3 setup.                                                    */

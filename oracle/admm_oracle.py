@@ -196,8 +196,12 @@ def _psf_centered_spectrum(kern: torch.Tensor, H: int, W: int) -> torch.Tensor:
 
 
 def solve_fourier(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool = False,
-                  maxit: int = 100, return_state: bool = False):
-    """Fourier-domain restatement (b once, roll differences) in xin's dtype."""
+                  maxit: int = 100, return_state: bool = False, norm_allreduce=None):
+    """Fourier-domain restatement (b once, roll differences) in xin's dtype.
+
+    norm_allreduce (iso only; test hook for a batch sharded over ranks): called every iteration
+    with the local per-pixel sums over (B, C) of a_x^2 and a_y^2 as one (2, H, W) tensor, which it
+    must replace in place by the sums over all ranks -- the contract of admm_tv_desc.allreduce."""
     B, C, H, W = xin.shape
     dt = xin.dtype
     lmbd = torch.as_tensor(lmbd, dtype=dt)
@@ -225,6 +229,16 @@ def solve_fourier(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool = 
         return a - torch.roll(a, -1, dims=2)
 
     shrink = shrink_block if iso else shrink_soft
+    if iso and norm_allreduce is not None:
+        def shrink_pair(ax, ay, tau):
+            sums = torch.stack([torch.sum(ax * ax, dim=(0, 1)), torch.sum(ay * ay, dim=(0, 1))])
+            norm_allreduce(sums)
+            fx = torch.clamp_min(1.0 - tau / (torch.sqrt(sums[0] + 1e-15) + 1e-15), 0.0)
+            fy = torch.clamp_min(1.0 - tau / (torch.sqrt(sums[1] + 1e-15) + 1e-15), 0.0)
+            return fx * ax, fy * ay
+    else:
+        def shrink_pair(ax, ay, tau):
+            return shrink(ax, tau), shrink(ay, tau)
     x = torch.zeros_like(xin)
     ux = torch.zeros_like(xin)
     uy = torch.zeros_like(xin)
@@ -235,8 +249,7 @@ def solve_fourier(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool = 
         x = torch.fft.irfftn(fc * torch.fft.rfftn(r, dim=(2, 3)), s=(H, W), dim=(2, 3))
         ax = Dx(x) + ux
         ay = Dy(x) + uy
-        zx = shrink(ax, tau)
-        zy = shrink(ay, tau)
+        zx, zy = shrink_pair(ax, ay, tau)
         ux = ax - zx
         uy = ay - zy
         wx = zx - ux

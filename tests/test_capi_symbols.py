@@ -49,7 +49,7 @@ def test_library_is_gfx950_code():
 def test_host_entry_points():
     from admmtor import _native
     lib = _native.load()
-    assert lib.admm_tv_abi_version() == 3
+    assert lib.admm_tv_abi_version() == 4
     fast, generic = 1, 2
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
     assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 4096), (8, 64), (1, 1), (481, 321))] == [generic] * 5
@@ -77,6 +77,20 @@ def test_host_error_codes(field, value, code):
     assert _native.load().admm_tv_last_error()
 
 
+def test_empty_shard_needs_an_iso_hook():
+    """B*C = 0 is invalid for a plain solve, valid for an iso solve with a cross-rank hook (an empty
+    shard still takes part in every all-reduce; ABI v4 carries the hook in the descriptor)."""
+    from admmtor import _native
+    lib = _native.load()
+    n = ctypes.c_size_t(0)
+    d = _native.desc(0, 3, 64, 64, 0, True, 5)
+    assert lib.admm_tv_workspace_size(ctypes.byref(d), ctypes.byref(n)) == -1
+    d.allreduce = _native.ALLREDUCE_FN(lambda *a: None)
+    assert lib.admm_tv_workspace_size(ctypes.byref(d), ctypes.byref(n)) == 0 and n.value >= 2 * 64 * 64 * 4
+    d.iso = 0  # the hook is only for iso
+    assert lib.admm_tv_workspace_size(ctypes.byref(d), ctypes.byref(n)) == -1
+
+
 def test_psf_larger_than_image_is_rejected():
     from admmtor import _native
     d = _native.desc(1, 1, 16, 16, 21, False, 5)
@@ -99,3 +113,10 @@ def test_groups_descriptor():
     assert lib.admm_tv_workspace_size(ctypes.byref(_native.desc(1, 1, 15, 17, 0, False, 5, 0, 2)), ctypes.byref(n)) == -2
     assert lib.admm_tv_workspace_size(ctypes.byref(_native.desc(1, 1, 64, 64, 3, False, 5, 1, 2)), ctypes.byref(n)) == -2
     assert lib.admm_tv_workspace_size(ctypes.byref(_native.desc(1, 1, 64, 64, 0, False, 5, 0, -1)), ctypes.byref(n)) == -1
+
+
+def test_library_built_from_this_tree():
+    """admm_tv_build_hash() (embedded by csrc/Makefile) equals the hash of the sources in the tree,
+    so a stale prebuilt library cannot pass for the current code (load() refuses it too)."""
+    from admmtor import _native
+    assert _native.load().admm_tv_build_hash().decode() == _native.source_hash()

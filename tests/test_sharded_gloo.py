@@ -69,6 +69,69 @@ def test_sharded_gloo_world2():
         assert err < 1e-6  # params broadcast as fp32: 1e-8-level differences only
 
 
+def _iso_worker(rank, world, port, B, q):
+    """iso over ranks through the real Python hook contract: the injected solver (the fp64 oracle)
+    hands its per-pixel sums to the per-call callback admm_tv_desc.allreduce would get
+    (AllReduceHook.bind -> ctypes callback -> view of the bound buffer -> dist.all_reduce)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "torch-admm-deconv_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from admmtor import _native
+        from admmtor.sharded import shard_bounds, sharded_fft_admm_tv
+        from admmtor.synth import blurred_batch, make_psf
+        from oracle.admm_oracle import solve_fourier
+        psf = make_psf("gauss:1.5", 5).double()
+        full = blurred_batch(B, 3, 16, 32, psf.float(), seed=4).double()
+        s, e = shard_bounds(B, world, rank)
+        hook = _native.AllReduceHook()
+        calls = []
+
+        def norm_allreduce(sums):
+            buf = sums.reshape(-1).float().contiguous()          # the library's fp32 2*H*W buffer
+            bound = hook.bind(buf)
+            bound.cfn(buf.data_ptr(), buf.numel(), None, None)   # as the C library calls it
+            bound.check()
+            sums.copy_(buf.reshape(sums.shape).double())
+            calls.append(1)
+
+        def solver(x, l, r, k, iso, it):
+            if x.shape[0] == 0:  # what the library does for an empty shard: zeros into every reduction
+                for _ in range(it):
+                    norm_allreduce(torch.zeros((2,) + tuple(x.shape[2:]), dtype=torch.float64))
+                return torch.zeros(x.shape, dtype=torch.float64)
+            return solve_fourier(x, l.double(), r.double(), k.double(), iso, it, norm_allreduce=norm_allreduce)
+
+        out = sharded_fft_admm_tv(full[s:e], 0.03, 0.05, psf.float(), True, 9, gather="all", solver=solver)
+        ref = solve_fourier(full, 0.03, 0.05, psf, True, 9)
+        q.put((rank, ((out.double() - ref).norm() / ref.norm()).item(), tuple(out.shape), len(calls), e - s))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B", [3, 1])
+def test_sharded_iso_hook_contract_gloo_world2(B):
+    """B = 3: shards of 2 and 1 images; B = 1: rank 1's shard is EMPTY and must still take part in
+    every iteration's all-reduce (else rank 0 hangs)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_iso_worker, args=(r, world, port, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    for rank, err, shape, ncalls, nloc in res:
+        assert shape == (B, 3, 16, 32)
+        assert ncalls == 9  # one reduction per iteration on every rank, empty shard included
+        assert err < 1e-6, (rank, err)  # sums carried as fp32 through the hook: 1e-8-level only
+
+
 def test_shard_bounds_cover_exactly():
     from admmtor.sharded import shard_bounds
     for total in (1, 7, 64, 512):

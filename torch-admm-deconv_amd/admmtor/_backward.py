@@ -16,9 +16,8 @@ spectrum (4 B/pixel/iteration more history) and is only enabled when the PSF req
 """
 from __future__ import annotations
 
-import contextlib
-
 import torch
+from torch.autograd.function import once_differentiable
 
 from . import _native
 
@@ -42,7 +41,9 @@ class AdmmTvFunction(torch.autograd.Function):
         G = lam.numel()  # > 1: modules sharing x32 (fft_admm_tv_grouped); output (G B, C, H, W)
         k = int(k32.shape[-1]) if k32.numel() > 0 else 0
         flags = _native.ADMM_TV_FLAG_PSF_GRAD if (psf_grad and k > 0) else 0
-        d = _native.desc(B, C, H, W, k, iso, maxit, flags, G)
+        hook = hook if iso else None
+        bound = hook.bind() if hook is not None else None
+        d = _native.desc(B, C, H, W, k, iso, maxit, flags, G, bound)
         x32 = x32.contiguous()
         k32c = k32.contiguous()
         lam_c, rho_c = lam.contiguous(), rho.contiguous()
@@ -50,13 +51,14 @@ class AdmmTvFunction(torch.autograd.Function):
         hist = torch.empty(max(_native.history_size(d), 1), dtype=torch.uint8, device=x32.device)
         out = torch.empty((G * B, C, H, W), dtype=torch.float32, device=x32.device)
         stream = torch.cuda.current_stream(x32.device).cuda_stream
-        hook = hook if iso else None
-        with (hook if hook is not None else contextlib.nullcontext()):
-            _native.register_buffers(ws, hist)
-            _native.check(lib.admm_tv_forward_train(
-                d, x32.data_ptr(), k32c.data_ptr() if k > 0 else None, lam_c.data_ptr(), rho_c.data_ptr(),
-                out.data_ptr(), hist.data_ptr(), hist.numel(), ws.data_ptr(), ws.numel(), stream))
-        del ws
+        if bound is not None:
+            bound.add(ws, hist)
+        _native.check(lib.admm_tv_forward_train(
+            d, x32.data_ptr(), k32c.data_ptr() if k > 0 else None, lam_c.data_ptr(), rho_c.data_ptr(),
+            out.data_ptr(), hist.data_ptr(), hist.numel(), ws.data_ptr(), ws.numel(), stream))
+        if bound is not None:
+            bound.check()
+        del ws, bound
         ctx.hook = hook
         ctx.save_for_backward(k32c, lam_c, rho_c, x32 if flags else None)
         ctx.hist = hist
@@ -64,10 +66,15 @@ class AdmmTvFunction(torch.autograd.Function):
         return out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, gout):
+        if ctx.hist is None:
+            raise RuntimeError("admmtor: fft_admm_tv's native backward was already run for this graph and its "
+                               "history released; backward through it twice (retain_graph=True) is not supported")
         k32, lam, rho, x32 = ctx.saved_tensors
         B, C, H, W, k, iso, maxit, flags, G = ctx.desc
-        d = _native.desc(B, C, H, W, k, iso, maxit, flags, G)
+        bound = ctx.hook.bind() if ctx.hook is not None else None
+        d = _native.desc(B, C, H, W, k, iso, maxit, flags, G, bound)
         need_k = ctx.needs_input_grad[3] and k > 0
         if need_k and not flags:
             raise RuntimeError("admmtor: PSF gradient requested but the forward did not keep the spectra")
@@ -82,16 +89,18 @@ class AdmmTvFunction(torch.autograd.Function):
         gk = torch.empty((1, 1, k, k), dtype=torch.float32, device=dev) if need_k else None
         ws = torch.empty(_native.backward_workspace_size(d), dtype=torch.uint8, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
-        with (ctx.hook if ctx.hook is not None else contextlib.nullcontext()):
-            _native.register_buffers(ws, ctx.hist)
-            _native.check(lib.admm_tv_backward(
-                d, x32.data_ptr() if x32 is not None else None, k32.data_ptr() if k > 0 else None,
-                lam.data_ptr(), rho.data_ptr(), g.data_ptr(), ctx.hist.data_ptr(), ctx.hist.numel(),
-                gx.data_ptr() if gx is not None else None,
-                gl.data_ptr() if gl is not None else None,
-                gr.data_ptr() if gr is not None else None,
-                gk.data_ptr() if gk is not None else None,
-                ws.data_ptr(), ws.numel(), stream))
+        if bound is not None:
+            bound.add(ws, ctx.hist)
+        _native.check(lib.admm_tv_backward(
+            d, x32.data_ptr() if x32 is not None else None, k32.data_ptr() if k > 0 else None,
+            lam.data_ptr(), rho.data_ptr(), g.data_ptr(), ctx.hist.data_ptr(), ctx.hist.numel(),
+            gx.data_ptr() if gx is not None else None,
+            gl.data_ptr() if gl is not None else None,
+            gr.data_ptr() if gr is not None else None,
+            gk.data_ptr() if gk is not None else None,
+            ws.data_ptr(), ws.numel(), stream))
+        if bound is not None:
+            bound.check()
         ctx.hist = None  # release the history as soon as the gradient is formed
         return (gx,
                 gl if ctx.needs_input_grad[1] else None,

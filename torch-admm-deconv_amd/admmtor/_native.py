@@ -6,6 +6,8 @@ library is missing or fails to load, every entry point raises loudly.
 from __future__ import annotations
 
 import ctypes
+import glob
+import hashlib
 import os
 import threading
 
@@ -23,6 +25,7 @@ ADMM_TV_EKERNEL = -6
 # every symbol include/admm_tv.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = (
     "admm_tv_abi_version",
+    "admm_tv_build_hash",
     "admm_tv_supported",
     "admm_tv_workspace_size",
     "admm_tv_forward",
@@ -31,7 +34,6 @@ EXPORTED = (
     "admm_tv_forward_train",
     "admm_tv_backward_workspace_size",
     "admm_tv_backward",
-    "admm_tv_set_allreduce",
     "admm_tv_profile_enable",
     "admm_tv_profile_reset",
     "admm_tv_profile_read",
@@ -50,6 +52,10 @@ EXPORTED_CHANSTAT = (
 CHANSTAT_F32, CHANSTAT_BF16, CHANSTAT_F16 = 0, 1, 2
 
 
+# admm_tv_allreduce_fn: (float* buf, size_t count, void* stream, void* ctx)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
+
+
 class AdmmTvDesc(ctypes.Structure):
     _fields_ = [
         ("B", ctypes.c_int64),
@@ -62,14 +68,13 @@ class AdmmTvDesc(ctypes.Structure):
         ("maxit", ctypes.c_int32),
         ("flags", ctypes.c_int32),
         ("groups", ctypes.c_int32),
+        ("allreduce", ALLREDUCE_FN),      # per-call cross-rank hook (iso over a sharded batch)
+        ("allreduce_ctx", ctypes.c_void_p),
     ]
 
 
 ADMM_TV_FLAG_PSF_GRAD = 1
-ABI_VERSION = 3
-
-
-ALLREDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
+ABI_VERSION = 4
 
 
 class NativeError(RuntimeError):
@@ -80,6 +85,22 @@ class NativeError(RuntimeError):
 
 _lib = None
 _lock = threading.Lock()
+
+_CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+
+
+def source_hash():
+    """The hash csrc/Makefile embeds (admm_tv_build_hash): SHA-256 of the library's sources in
+    byte-wise sorted path order, then the Makefile; None when the sources are not in the tree."""
+    if not os.path.isfile(os.path.join(_CSRC, "Makefile")):
+        return None
+    rel = sorted(glob.glob("*.hip", root_dir=_CSRC) + glob.glob("*.hpp", root_dir=_CSRC)
+                 + glob.glob("../../include/*.h", root_dir=_CSRC), key=lambda p: p.encode())
+    h = hashlib.sha256()
+    for r in rel + ["Makefile"]:
+        with open(os.path.join(_CSRC, r), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def lib_path() -> str:
@@ -104,6 +125,8 @@ def load() -> ctypes.CDLL:
         dp = ctypes.POINTER(AdmmTvDesc)
         L.admm_tv_abi_version.restype = ctypes.c_int
         L.admm_tv_abi_version.argtypes = []
+        L.admm_tv_build_hash.restype = ctypes.c_char_p
+        L.admm_tv_build_hash.argtypes = []
         L.admm_tv_supported.restype = ctypes.c_int
         L.admm_tv_supported.argtypes = [ctypes.c_int64, ctypes.c_int64]
         L.admm_tv_workspace_size.restype = ctypes.c_int
@@ -120,8 +143,6 @@ def load() -> ctypes.CDLL:
         L.admm_tv_backward.argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, sz, vp]
         L.admm_tv_psf_transpose.restype = ctypes.c_int
         L.admm_tv_psf_transpose.argtypes = [dp, vp, vp, vp, vp, sz, vp]
-        L.admm_tv_set_allreduce.restype = ctypes.c_int
-        L.admm_tv_set_allreduce.argtypes = [ALLREDUCE_FN, vp]
         L.admm_tv_profile_enable.restype = ctypes.c_int
         L.admm_tv_profile_enable.argtypes = [ctypes.c_int]
         L.admm_tv_profile_reset.restype = ctypes.c_int
@@ -147,6 +168,10 @@ def load() -> ctypes.CDLL:
         L.admm_planestat_select.argtypes = [ctypes.c_int, vp, i64, i64, vp, vp, vp, vp, sz, ctypes.c_int, vp]
         if L.admm_tv_abi_version() != ABI_VERSION:
             raise ImportError("admmtor: native library ABI version mismatch")
+        want, have = source_hash(), L.admm_tv_build_hash().decode()
+        if want is not None and want != have:
+            raise ImportError(f"admmtor: {_LIB_PATH} was built from other sources (build hash {have}, tree "
+                              f"{want}); rebuild it: `python __graft_entry__.py build`")
         _lib = L
         return L
 
@@ -157,9 +182,10 @@ def check(code: int) -> None:
         raise NativeError(code, msg)
 
 
-def desc(B, C, H, W, k, iso, maxit, flags=0, groups=1) -> AdmmTvDesc:
+def desc(B, C, H, W, k, iso, maxit, flags=0, groups=1, allreduce=None) -> AdmmTvDesc:
+    """allreduce: a BoundAllReduce (AllReduceHook.bind) for iso over a sharded batch, or None."""
     return AdmmTvDesc(int(B), int(C), int(H), int(W), int(k), int(k), int(bool(iso)), int(maxit), int(flags),
-                      int(groups))
+                      int(groups), allreduce.cfn if allreduce is not None else ALLREDUCE_FN(), None)
 
 
 def workspace_size(d: AdmmTvDesc) -> int:
@@ -185,48 +211,59 @@ def supported(H: int, W: int) -> bool:
 
 
 # --------------------------------------------------------------------------- cross-rank hook
-# Device buffers the library may hand to the all-reduce callback live inside tensors the
-# Python side allocated (workspace, history); the callback maps the raw pointer back to a
-# view of one of them.
-_live_buffers = []
+class BoundAllReduce:
+    """The all-reduce callback of ONE native call (admm_tv_desc.allreduce).  The library hands it
+    raw device pointers inside the buffers this call allocated (workspace, history); they are
+    mapped back to views of exactly those tensors.  Nothing is shared between calls, so solves on
+    several threads / streams each carry their own.  A Python exception inside the callback
+    cannot cross the C frame: it is kept and re-raised by check() after the call returns."""
 
+    def __init__(self, dist, group, tensors=()):
+        self._dist, self._group = dist, group
+        self._bufs = []
+        self.add(*tensors)
+        self.error = None
+        self.cfn = ALLREDUCE_FN(self._call)  # referenced by self for the duration of the call
 
-def register_buffers(*tensors):
-    _live_buffers[:] = [t for t in tensors if t is not None]
+    def add(self, *tensors):
+        """Buffers of this call the library may hand to the callback (workspace, history)."""
+        self._bufs.extend(t for t in tensors if t is not None)
 
+    def _view_of(self, ptr: int, count: int):
+        import torch
+        nbytes = 4 * count
+        for t in self._bufs:
+            base = t.data_ptr()
+            if base <= ptr and ptr + nbytes <= base + t.numel() * t.element_size():
+                off = ptr - base
+                return t.view(torch.uint8)[off:off + nbytes].view(torch.float32)
+        raise RuntimeError("admmtor: all-reduce buffer not inside this call's workspace")
 
-def _view_of(ptr: int, count: int):
-    import torch
-    nbytes = 4 * count
-    for t in _live_buffers:
-        base = t.data_ptr()
-        if base <= ptr and ptr + nbytes <= base + t.numel() * t.element_size():
-            off = ptr - base
-            return t.view(torch.uint8)[off:off + nbytes].view(torch.float32)
-    raise RuntimeError("admmtor: all-reduce buffer not inside a registered workspace")
+    def _call(self, ptr, count, stream, ctx):
+        if self.error is not None:
+            return
+        try:
+            self._dist.all_reduce(self._view_of(int(ptr), int(count)), op=self._dist.ReduceOp.SUM,
+                                  group=self._group)
+        except BaseException as e:  # noqa: BLE001 -- re-raised by check()
+            self.error = e
+
+    def check(self):
+        if self.error is not None:
+            raise RuntimeError("admmtor: cross-rank all-reduce failed inside the solve") from self.error
 
 
 class AllReduceHook:
-    """Context manager installing a SUM all-reduce (torch.distributed) for iso sharding."""
+    """SUM all-reduce over a torch.distributed group for iso over a sharded batch.  bind() makes
+    the per-call callback; the hook itself holds no per-solve state."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
         self._dist = dist
         self._group = group
-        self._cb = ALLREDUCE_FN(self._call)
 
-    def _call(self, ptr, count, stream, ctx):
-        t = _view_of(int(ptr), int(count))
-        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self._group)
-
-    def __enter__(self):
-        check(load().admm_tv_set_allreduce(self._cb, None))
-        return self
-
-    def __exit__(self, *exc):
-        check(load().admm_tv_set_allreduce(ALLREDUCE_FN(), None))
-        register_buffers()
-        return False
+    def bind(self, *tensors) -> BoundAllReduce:
+        return BoundAllReduce(self._dist, self._group, tensors)
 
 
 def profile_enable(on: bool) -> None:

@@ -15,7 +15,6 @@ Drop-in for ``/root/reference/src/admmtor/eops/deconv.py``:
 """
 from __future__ import annotations
 
-import contextlib
 from typing import Tuple
 
 import torch
@@ -111,22 +110,26 @@ def _as_device_scalar(v, device) -> torch.Tensor:
 def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.Tensor, iso: bool, maxit: int,
            hook=None):
     """Run the HIP solver: x32 (B,C,H,W) fp32 contiguous on the device -> new tensor.
-    `hook`: an _native.AllReduceHook for iso over a batch sharded across ranks."""
+    `hook`: an _native.AllReduceHook for iso over a batch sharded across ranks; its callback is
+    bound to this call's workspace only (no process-global state)."""
     lib = _native.load()
     B, C, H, W = x32.shape
     G = lam.numel()  # modules solved together (fft_admm_tv_grouped); 1 for fft_admm_tv
     k = int(k32.shape[-1]) if k32.numel() > 0 else 0
-    d = _native.desc(B, C, H, W, k, iso, maxit, 0, G)
+    bound = hook.bind() if (hook is not None and iso) else None
+    d = _native.desc(B, C, H, W, k, iso, maxit, 0, G, bound)
     if not _native.supported(H, W):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} outside [1, 4096]")
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
+    if bound is not None:
+        bound.add(ws)
     out = torch.empty((G * B, C, H, W), dtype=torch.float32, device=x32.device)
     stream = torch.cuda.current_stream(x32.device).cuda_stream
-    with (hook if (hook is not None and iso) else contextlib.nullcontext()):
-        _native.register_buffers(ws)
-        _native.check(lib.admm_tv_forward(
-            d, x32.data_ptr(), k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(),
-            out.data_ptr(), ws.data_ptr(), ws.numel(), stream))
+    _native.check(lib.admm_tv_forward(
+        d, x32.data_ptr(), k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(),
+        out.data_ptr(), ws.data_ptr(), ws.numel(), stream))
+    if bound is not None:
+        bound.check()
     return out
 
 
@@ -157,7 +160,10 @@ def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> 
         raise RuntimeError("admmtor (MI355X build): fft_admm_tv runs on ROCm device tensors only; "
                            "move xin (and kern) to the GPU. There is no CPU path.")
     maxit = max(0, int(maxit))  # the reference loops over torch.arange(0, maxit): negative -> no iteration
-    if xin.numel() == 0:  # empty batch: the reference's ops return an empty result of the same shape
+    # empty batch: the reference's ops return an empty result of the same shape.  An empty shard of
+    # an iso solve over ranks still runs: it must take part in every iteration's all-reduce.
+    shard_member = hook is not None and iso and xin.shape[2] > 0 and xin.shape[3] > 0
+    if xin.numel() == 0 and not shard_member:
         return torch.zeros(xin.shape, dtype=torch.float32, device=xin.device)
     dev = xin.device
     x32 = xin.detach().to(torch.float32).contiguous()

@@ -6,8 +6,9 @@ communication.  The only collectives are a broadcast of the PSF, lambda and rho
 from rank 0 (a few KB: every rank then builds its own Wiener factor) and,
 optionally, a final gather of the outputs.  iso=True couples the whole batch
 through the per-pixel (B, C) norm: it is sharded with a per-iteration SUM
-all-reduce of the 2*H*W per-pixel sums (RCCL), installed through the C ABI hook
-``admm_tv_set_allreduce`` (and of the cross-plane products Q in the backward).
+all-reduce of the 2*H*W per-pixel sums (RCCL), handed to the library per call in the
+descriptor (``admm_tv_desc.allreduce``; also the cross-plane products Q in the backward).  A rank
+whose shard is empty (B < world) still takes part in every one of those reductions.
 
 The reference has no distributed code at all; this module is the
 multi-GPU layer of the MI355X build.

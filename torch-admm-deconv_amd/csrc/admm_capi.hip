@@ -9,6 +9,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -32,7 +33,10 @@ struct ProfRec {
     int kind;
     hipEvent_t a, b;
 };
+// process-wide totals (bench.py reads them); every access holds g_prof.mu, so solves on
+// several threads / streams may record concurrently
 struct Prof {
+    std::mutex mu;
     bool on = false;
     std::vector<ProfRec> recs;
     std::vector<hipEvent_t> pool;
@@ -40,7 +44,7 @@ struct Prof {
     int64_t n[4] = {0, 0, 0, 0};
 } g_prof;
 
-hipEvent_t prof_event() {
+hipEvent_t prof_event() {  // caller holds g_prof.mu
     if (!g_prof.pool.empty()) {
         hipEvent_t e = g_prof.pool.back();
         g_prof.pool.pop_back();
@@ -56,6 +60,7 @@ struct ProfScope {
     hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
     ProfScope(int k, hipStream_t st) : kind(k), s(st) {
+        std::lock_guard<std::mutex> lk(g_prof.mu);
         if (g_prof.on) {
             a = prof_event();
             b = prof_event();
@@ -65,17 +70,18 @@ struct ProfScope {
     ~ProfScope() {
         if (a && b) {
             (void)hipEventRecord(b, s);
+            std::lock_guard<std::mutex> lk(g_prof.mu);
             g_prof.recs.push_back({kind, a, b});
         }
     }
 };
 
-// ------------------------------------------------------------------ cross-rank reduction hook (iso)
-typedef void (*allreduce_fn)(float* buf, size_t count, void* stream, void* ctx);
-struct AllReduce {
-    allreduce_fn fn = nullptr;
-    void* ctx = nullptr;
-} g_allreduce;
+// cross-rank reduction hook (iso): carried per call in the descriptor (admm_tv_desc.allreduce)
+void allreduce(const admm_tv_desc& d, float* buf, size_t count, hipStream_t s) {
+    if (d.allreduce) d.allreduce(buf, count, s, d.allreduce_ctx);
+}
+// an empty shard of an iso solve over ranks: only its part of the reductions remains
+bool participate_only(const admm_tv_desc& d) { return d.iso && d.allreduce && d.B * d.C == 0; }
 
 // ------------------------------------------------------------------ geometry
 bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
@@ -373,7 +379,9 @@ int xspec(int H, const cf* U, const cf* V, cf* part, const cf* twH, int N, int P
 
 int validate(const admm_tv_desc* d) {
     if (!d) return fail(ADMM_TV_EINVAL, "null descriptor");
-    if (d->B <= 0 || d->C <= 0 || d->H <= 0 || d->W <= 0 || d->maxit < 0 || d->kh < 0 || d->kw < 0 || d->groups < 0)
+    const bool empty_ok = d->iso && d->allreduce && d->B >= 0 && d->C >= 0;  // see participate_only
+    if ((empty_ok ? (d->B < 0 || d->C < 0) : (d->B <= 0 || d->C <= 0)) || d->H <= 0 || d->W <= 0 || d->maxit < 0 ||
+        d->kh < 0 || d->kw < 0 || d->groups < 0)
         return fail(ADMM_TV_EINVAL, "invalid sizes or maxit");
     if (d->kh != d->kw) return fail(ADMM_TV_ENONSQUARE, "non-square PSF (the reference's H_t swaps H/W pads)");
     if (!supported_hw(d->H, d->W) && !generic_hw(d->H, d->W))
@@ -415,8 +423,13 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
     return 0;
 }
 
+int pow2_floor(int v);
+
 int strip_rows(int H, int N, long long rows, bool aniso_fwd = false) {
     int R = env_int("ADMM_PASSA_R", 0);
+    // A/B knob: a strip must tile H exactly (pass A maps strip -> (plane, first row) by H / R),
+    // so an override is rounded down to a power of two in [2, H]; <= 0 selects the rule below
+    if (R > 0) R = pow2_floor(std::max(2, std::min(R, H)));
     if (R <= 0) {
         // rows per strip (measured on MI355X, tools/sweep.py: R = 8 beats 16 at W = 1024 with
         // the 3-waves/SIMD row pass); halve while there are fewer than ~3 waves per SIMD of
@@ -686,7 +699,7 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, c
             else
                 hipLaunchKernelGGL((k_giso_norm<false, false>), grid, blk, 0, s, xk, uxi, uyi, nprev, lam, rho, nout, H, W, P);
             if (int e = launch_check("k_giso_norm")) return e;
-            if (g_allreduce.fn) g_allreduce.fn(nout, 2ull * H * W, s, g_allreduce.ctx);
+            allreduce(d, nout, 2ull * H * W, s);
             nsq = nout;
         }
         {
@@ -714,7 +727,16 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     const int H = (int)d.H, W = (int)d.W, N = W / 2;
     const size_t img_bytes = (size_t)P * H * W * sizeof(float);
     if (d.maxit == 0) {
-        HIPCHK(hipMemsetAsync(out, 0, img_bytes, s));  // the reference returns x = zeros (deconv.py:61,117)
+        if (img_bytes) HIPCHK(hipMemsetAsync(out, 0, img_bytes, s));  // the reference returns x = zeros (deconv.py:61,117)
+        return 0;
+    }
+    if (participate_only(d)) {  // the same reductions as run_forward's iso loop, contributing zeros
+        const size_t n = (size_t)G * 2 * H * W;
+        for (int it = 1; it <= d.maxit; ++it) {
+            if (it == d.maxit && !hist) break;
+            HIPCHK(hipMemsetAsync(at<float>(ws, Lo.nsq), 0, n * sizeof(float), s));
+            allreduce(d, at<float>(ws, Lo.nsq), Lo.gen ? 2ull * H * W : n, s);
+        }
         return 0;
     }
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
@@ -801,7 +823,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
                 if ((e = launch_check("k_iso_reduce"))) return e;
             }
             // sharded batch: the per-pixel sums must cover every rank's planes
-            if (g_allreduce.fn) g_allreduce.fn(nout, (size_t)G * 2 * H * W, s, g_allreduce.ctx);
+            allreduce(d, nout, (size_t)G * 2 * H * W, s);
             nsq = nout;
         }
         {
@@ -931,7 +953,7 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xi
             hipLaunchKernelGGL(k_iso_tau_partial, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
                                tpart + (size_t)(K - k) * BL.ntp, 2LL * HW);
             if (int e = launch_check("k_iso_tau_partial")) return e;
-            if (g_allreduce.fn) g_allreduce.fn(q, 2ull * H * W, s, g_allreduce.ctx);
+            allreduce(d, q, 2ull * H * W, s);
         }
         {
             ProfScope ps(0, s);
@@ -991,7 +1013,8 @@ int admm_tv_workspace_size(const admm_tv_desc* d, size_t* bytes) {
 int admm_tv_forward(const admm_tv_desc* dp, const float* xin, const float* kern, const float* lam, const float* rho,
                     float* out, void* ws, size_t ws_bytes, void* stream) {
     if (int e = validate(dp)) return e;
-    if (!xin || !out || !lam || !rho || (dp->kh > 0 && !kern)) return fail(ADMM_TV_EINVAL, "null pointer argument");
+    if (((!xin || !out) && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
+        return fail(ADMM_TV_EINVAL, "null pointer argument");
     return run_forward(*dp, xin, kern, lam, rho, out, ws, ws_bytes, nullptr, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -1006,7 +1029,8 @@ int admm_tv_forward_train(const admm_tv_desc* dp, const float* xin, const float*
                           const float* rho, float* out, void* hist, size_t hist_bytes, void* ws, size_t ws_bytes,
                           void* stream) {
     if (int e = validate(dp)) return e;
-    if (!xin || !out || !lam || !rho || (dp->kh > 0 && !kern)) return fail(ADMM_TV_EINVAL, "null pointer argument");
+    if (((!xin || !out) && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
+        return fail(ADMM_TV_EINVAL, "null pointer argument");
     if (dp->maxit > 0 && (!hist || hist_bytes < make_hist(*dp).total))
         return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
     return run_forward(*dp, xin, kern, lam, rho, out, ws, ws_bytes, dp->maxit > 0 ? hist : nullptr,
@@ -1026,7 +1050,8 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     if (int e = validate(dp)) return e;
     const admm_tv_desc d = *dp;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (!gout || !lam || !rho || (d.kh > 0 && !kern)) return fail(ADMM_TV_EINVAL, "null pointer argument");
+    if ((!gout && !participate_only(d)) || !lam || !rho || (d.kh > 0 && !kern))
+        return fail(ADMM_TV_EINVAL, "null pointer argument");
     const BwdLayout BL = make_bwd_layout(d);
     const Layout& Lo = BL.f;
     if (!ws || ws_bytes < BL.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
@@ -1036,10 +1061,21 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     const int H = (int)d.H, W = (int)d.W, N = W / 2, K = d.maxit;
     const size_t img_bytes = (size_t)Pm * H * W * sizeof(float);  // gxin: one module's planes
     const bool psf_grad = gkern != nullptr;
-    if (psf_grad && (d.kh == 0 || !(d.flags & ADMM_TV_FLAG_PSF_GRAD) || !xin))
+    if (psf_grad && (d.kh == 0 || !(d.flags & ADMM_TV_FLAG_PSF_GRAD) || (!xin && !participate_only(d))))
         return fail(ADMM_TV_EINVAL, "gkern needs a PSF, ADMM_TV_FLAG_PSF_GRAD (forward and backward) and xin");
     if (K == 0) {  // output is identically zero
         if (gxin) HIPCHK(hipMemsetAsync(gxin, 0, img_bytes, s));
+        if (glam) HIPCHK(hipMemsetAsync(glam, 0, sizeof(float) * G, s));
+        if (grho) HIPCHK(hipMemsetAsync(grho, 0, sizeof(float) * G, s));
+        if (gkern) HIPCHK(hipMemsetAsync(gkern, 0, sizeof(float) * d.kh * d.kw, s));
+        return 0;
+    }
+    if (participate_only(d)) {  // the same reductions as the iso backward below, contributing zeros
+        const size_t n = (size_t)G * 2 * H * W;
+        for (int k = K; k >= 2; --k) {
+            HIPCHK(hipMemsetAsync(at<float>(ws, BL.q), 0, n * sizeof(float), s));
+            allreduce(d, at<float>(ws, BL.q), Lo.gen ? 2ull * H * W : n, s);
+        }
         if (glam) HIPCHK(hipMemsetAsync(glam, 0, sizeof(float) * G, s));
         if (grho) HIPCHK(hipMemsetAsync(grho, 0, sizeof(float) * G, s));
         if (gkern) HIPCHK(hipMemsetAsync(gkern, 0, sizeof(float) * d.kh * d.kw, s));
@@ -1109,7 +1145,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
                                    tpart + ((size_t)(K - k) * G + g) * BL.ntp, 2LL * H * W);
                 if ((e = launch_check("k_iso_tau_partial"))) return e;
             }
-            if (g_allreduce.fn) g_allreduce.fn(q, (size_t)G * 2 * H * W, s, g_allreduce.ctx);
+            allreduce(d, q, (size_t)G * 2 * H * W, s);
         }
         {
             ProfScope ps(0, s);
@@ -1185,18 +1221,14 @@ int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float*
     return psf_transpose_into(d, Lo, ws, xin, out, at<cf>(ws, Lo.spec[0]), 1, s);
 }
 
-int admm_tv_set_allreduce(admm_tv_allreduce_fn fn, void* ctx) {
-    g_allreduce.fn = fn;
-    g_allreduce.ctx = ctx;
-    return 0;
-}
-
 int admm_tv_profile_enable(int enable) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
     g_prof.on = enable != 0;
     return 0;
 }
 
 int admm_tv_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
     for (auto& r : g_prof.recs) {
         (void)hipEventSynchronize(r.b);
         g_prof.pool.push_back(r.a);
@@ -1211,6 +1243,7 @@ int admm_tv_profile_reset(void) {
 }
 
 int admm_tv_profile_read(double* ms4, int64_t* count4) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
     for (auto& r : g_prof.recs) {
         if (hipEventSynchronize(r.b) != hipSuccess) return fail(ADMM_TV_EHIP, "hipEventSynchronize");
         float ms = 0.f;
