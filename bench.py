@@ -261,8 +261,10 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        # RCCL broadcast of PSF / lambda / rho from rank 0 (no-op at N=1), then the local shard
-        return sharded_fft_admm_tv(x, lam, rho, psf, iso, maxit)
+        # RCCL broadcast of PSF / lambda / rho from rank 0 (no-op at N=1), the local shard, and for
+        # N > 1 the north star's final gather of the whole output over xGMI (all_gather, RCCL)
+        return sharded_fft_admm_tv(x, lam, rho, psf, iso, maxit, gather="all" if world > 1 else None,
+                                   total_batch=B * world)
 
     for _ in range(args.warmup):
         out = step()
@@ -335,8 +337,11 @@ def main():
             "dtype": "f32",
             "data": "synthetic (piecewise-constant shapes, circular blur, AWGN 0.01; seeded per rank)",
             "config": {"workload": desc, "batch_per_gpu": B, "channels": C, "H": H, "W": W, "psf": f"{kind}/{k}",
-                       "maxit": maxit, "iso": iso, "parallelism": f"shard{world} (batch sharded, no data-path "
-                                                                  "collective)"},
+                       "maxit": maxit, "iso": iso,
+                       "parallelism": (f"shard{world} (batch sharded; RCCL broadcast of PSF/lambda/rho and a final "
+                                       "all_gather of the output inside the timed step"
+                                       + (", per-iteration all_reduce of the iso norms" if iso else "") + ")")
+                       if world > 1 else "shard1 (single GPU, no collective)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                          "traffic_source": traffic_src,

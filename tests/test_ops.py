@@ -1,0 +1,52 @@
+"""The dispatcher ops admm_hip::* on the CPU: registration, fake kernels, and a
+dynamo trace of ADMMDeconv with no graph break (meta tensors: shapes only, nothing runs).  The
+real kernels are checked with torch.library.opcheck on the GPU (tests/test_gpu_ops.py)."""
+import pytest
+import torch
+
+
+def test_ops_registered():
+    import admmtor._ops  # noqa: F401
+    for name in ("fft_admm_tv_fwd", "fft_admm_tv_fwd_train", "fft_admm_tv_bwd"):
+        assert hasattr(torch.ops.admm_hip, name)
+
+
+def test_fake_kernels_shapes():
+    import admmtor._ops  # noqa: F401
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from admmtor import _native
+    with FakeTensorMode():
+        x = torch.empty(2, 3, 64, 32)
+        lam = torch.empty(2)  # two modules solved together
+        k = torch.empty(1, 1, 5, 5)
+        assert torch.ops.admm_hip.fft_admm_tv_fwd(x, lam, lam, k, False, 10).shape == (4, 3, 64, 32)
+        out, hist = torch.ops.admm_hip.fft_admm_tv_fwd_train(x, lam, lam, k, True, 10, False)
+        assert out.shape == (4, 3, 64, 32) and hist.dtype == torch.uint8
+        want = _native.history_size(_native.desc(2, 3, 64, 32, 5, True, 10, 0, 2))
+        assert hist.shape == (want,)
+        gx, gl, gr, gk = torch.ops.admm_hip.fft_admm_tv_bwd(out, x, lam, lam, k, hist, True, 10, False,
+                                                             True, True, False)
+        assert gx.shape == x.shape and gl.shape == (2,) and gr.shape == (2,) and gk.numel() == 0
+
+
+def test_ops_refuse_host_tensors():
+    import admmtor._ops  # noqa: F401
+    x = torch.rand(1, 1, 16, 16)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        torch.ops.admm_hip.fft_admm_tv_fwd(x, torch.ones(1), torch.ones(1), torch.empty(0), False, 2)
+
+
+@pytest.mark.parametrize("iso,kern", [(False, (5, 5)), (True, ())])
+def test_admmdeconv_traces_as_one_graph(iso, kern):
+    from admmtor.elayers.admmdeconv import ADMMDeconv
+    torch._dynamo.reset()
+    m = ADMMDeconv(kern, 10, iso=iso).to("meta")
+    x = torch.empty(2, 3, 64, 64, device="meta", requires_grad=True)
+    ex = torch._dynamo.explain(m)(x)
+    assert ex.graph_count == 1 and ex.graph_break_count == 0, ex.break_reasons
+    code = ex.graphs[0].code
+    assert "admm_hip.fft_admm_tv_fwd_train" in code
+    y = torch.compile(m, backend="aot_eager", fullgraph=True)(x)
+    assert y.shape == x.shape
+    y.sum().backward()
+    assert x.grad.shape == x.shape

@@ -328,6 +328,71 @@ __global__ void __launch_bounds__(TPB) k_colmimic_t(cf* __restrict__ spec, int H
     for (int j = 0; j < 32; ++j) if (j < EE) { v[j].x *= 1.0001f; base[toff<T>(t + LL * j, cb * 8 + c)] = v[j]; }
 }
 
+
+// --- mixed layouts (round 2): pass A reads the x spectrum row-major and writes the r spectrum
+// column-tiled [P][H/T][N/8][T][8]; pass B reads tiled and writes row-major (out of place).
+__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
+    const unsigned x = b & 7u, i = b >> 3, q = nb >> 3, r = nb & 7u;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+#ifndef SO_NT
+#define SO_NT true
+#endif
+template <int R, int T>
+__global__ void __launch_bounds__(256) k_mimic_ot(const cf* __restrict__ sp, const cf* __restrict__ uxi,
+                                                  const cf* __restrict__ uyi, const cf* __restrict__ b,
+                                                  cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
+                                                  int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    cf acc[E];
+    for (int j = 0; j < E; ++j) acc[j] = ld(&sp[base + (size_t)((i0 - 1 + H) & (H - 1)) * N + t + L * j], true);
+    for (int rr = 0; rr <= R; ++rr) {
+        const int gi = (i0 + rr) & (H - 1), gm = (i0 + rr - 1 + H) & (H - 1);
+        const size_t ro = base + (size_t)gi * N;
+        const size_t rm = base + (size_t)gm * N;
+        cf x[E], uy[E];
+        for (int j = 0; j < E; ++j) x[j] = ld(&sp[ro + t + L * j], true);
+        for (int j = 0; j < E; ++j) { uy[j] = ld(&uyi[ro + t + L * j], true); uy[j].x += x[j].x; uy[j].y += acc[j].y; }
+        if (rr < R) for (int j = 0; j < E; ++j) st(&uyo[ro + t + L * j], uy[j], true);
+        if (rr >= 1) {
+            for (int j = 0; j < E; ++j) { cf bb = ld(&b[rm + t + L * j], true); acc[j].x += bb.x; acc[j].y -= bb.y; }
+            for (int j = 0; j < E; ++j) st(&so[base + toff<T>(gm, t + L * j)], acc[j], SO_NT);
+        }
+        if (rr < R) {
+            for (int j = 0; j < E; ++j) { cf u = ld(&uxi[ro + t + L * j], true); u.x -= x[j].y; u.y += x[j].x; st(&uxo[ro + t + L * j], u, true); }
+        }
+        for (int j = 0; j < E; ++j) acc[j] = x[j];
+    }
+}
+// pass B: 8 columns x all H rows per block; IN_T / OUT_T: tiled (T) or row-major input / output
+template <int TPB, int T, bool IN_T, bool OUT_T, bool REMAP>
+__global__ void __launch_bounds__(TPB) k_colmimic_mix(const cf* __restrict__ si, cf* __restrict__ so, int H, int colblocks) {
+    constexpr int C = 8, LL = TPB / C;
+    const int c = threadIdx.x % C, t = threadIdx.x / C;
+    const unsigned lb = REMAP ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int p = lb / colblocks, cb = lb % colblocks;
+    const size_t base = (size_t)p * H * N;
+    const int EE = H / LL;
+    cf v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < EE) {
+        const int r = t + LL * j, col = cb * 8 + c;
+        v[j] = si[base + (IN_T ? toff<T>(r, col) : (size_t)r * N + col)];
+    }
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < EE) {
+        const int r = t + LL * j, col = cb * 8 + c;
+        v[j].x *= 1.0001f;
+        so[base + (OUT_T ? toff<T>(r, col) : (size_t)r * N + col)] = v[j];
+    }
+}
+
 int main() {
     const int P = 192, H = 1024;
     const size_t n = (size_t)P * H * N;  // cf per array
@@ -353,6 +418,24 @@ int main() {
         printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
     const double arr = (double)n * sizeof(cf);
+    if (getenv("MIXED_SWEEP")) {
+        const long long ns = (long long)P * H / 8;
+        const int colblocks = N / 8;
+        for (int rep = 0; rep < 3; ++rep) {
+            timeit("A row-major nt (prod) R=8", 7 * arr, [&] { k_mimic<8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A out-tiled T=8 R=8", 7 * arr, [&] { k_mimic_ot<8, 8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A out-tiled T=16 R=8", 7 * arr, [&] { k_mimic_ot<8, 16><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A out-tiled T=4 R=8", 7 * arr, [&] { k_mimic_ot<8, 4><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("B row->row remap (prod, oop)", 2 * arr, [&] { k_colmimic_mix<512, 8, false, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+            timeit("B tiled8->row remap", 2 * arr, [&] { k_colmimic_mix<512, 8, true, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+            timeit("B tiled8->row noremap", 2 * arr, [&] { k_colmimic_mix<512, 8, true, false, false><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+            timeit("B tiled16->row remap", 2 * arr, [&] { k_colmimic_mix<512, 16, true, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+            timeit("B tiled4->row remap", 2 * arr, [&] { k_colmimic_mix<512, 4, true, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+            timeit("B tiled8->tiled8 remap", 2 * arr, [&] { k_colmimic_mix<512, 8, true, true, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+            timeit("copy float4", 2 * arr, [&] { k_copy<false><<<16384, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
+        }
+        return 0;
+    }
     if (getenv("TILE_SWEEP")) {
         const long long ns = (long long)P * H / 8;
         for (int rep = 0; rep < 2; ++rep) {

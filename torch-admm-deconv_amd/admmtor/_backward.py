@@ -13,6 +13,10 @@ through the Wiener factor, using dM/drho = -M D^T D M) and the PSF (through b = 
 and through |sigma|^2 in the Wiener factor: a per-frequency cross-spectrum accumulated over
 planes and iterations, csrc/admm_backward.hpp).  The PSF path keeps each iteration's r_k
 spectrum (4 B/pixel/iteration more history) and is only enabled when the PSF requires grad.
+
+The normal path goes through the dispatcher ops of ``admmtor._ops`` (autograd registered on
+``admm_hip::fft_admm_tv_fwd_train``).  This ``autograd.Function`` carries only the sharded iso
+solve, whose per-call all-reduce hook (a Python callable) cannot be an op argument.
 """
 from __future__ import annotations
 
@@ -118,15 +122,3 @@ def fft_admm_tv_autograd(xin, lmbd, rho, kern, iso, maxit, hook=None):
     psf_grad = isinstance(kern, torch.Tensor) and kern.requires_grad and kern.numel() > 0
     out = AdmmTvFunction.apply(x32, lam_t, rho_t, k32, bool(iso), int(maxit), hook, psf_grad)
     return out
-
-
-def fft_admm_tv_grouped_autograd(xin, lmbds, rhos, kern, iso, maxit):
-    """G modules sharing xin (eops.deconv.fft_admm_tv_grouped) with the native backward: lambda and
-    rho are stacked into (G,) tensors (differentiably, so each module's parameters get theirs)."""
-    dev = xin.device
-    x32 = xin.to(torch.float32)
-    k32 = kern.detach().to(device=dev, dtype=torch.float32) if kern.numel() > 0 else \
-        torch.empty(0, dtype=torch.float32, device=dev)
-    lam_t = torch.cat([_scalar_input(v, dev)[0] for v in lmbds])
-    rho_t = torch.cat([_scalar_input(v, dev)[0] for v in rhos])
-    return AdmmTvFunction.apply(x32, lam_t, rho_t, k32, bool(iso), int(maxit), None, False)

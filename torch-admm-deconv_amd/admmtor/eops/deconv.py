@@ -21,6 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _native
+from .. import _ops  # noqa: F401  (registers the admm_hip::* dispatcher ops)
 
 __all__ = [
     "torch_abs2",
@@ -94,9 +95,6 @@ def _check_inputs(xin: torch.Tensor, kern: torch.Tensor):
                                f"(deconv.py:90-96) and fail for shape {tuple(kern.shape)}")
         if not autocast and kern.dtype != xin.dtype:
             raise RuntimeError(f"expected kern dtype {xin.dtype}, got {kern.dtype}")
-    if xin.dtype == torch.float64:
-        raise RuntimeError("admmtor (MI355X build): fp64 inputs are not supported by the HIP kernels; "
-                           "pass float32 (or bf16/fp16 under torch.autocast)")
 
 
 def _as_device_scalar(v, device) -> torch.Tensor:
@@ -107,29 +105,57 @@ def _as_device_scalar(v, device) -> torch.Tensor:
     return torch.full((1,), float(v), dtype=torch.float32, device=device)
 
 
+def _scalar_input(v, device) -> torch.Tensor:
+    """lmbd / rho -> fp32 (1,) device tensor; differentiable when v is a tensor that requires grad."""
+    if isinstance(v, torch.Tensor):
+        if v.numel() != 1:
+            raise NotImplementedError("lmbd / rho must be scalars or 1-element tensors")
+        return v.reshape(1).to(device=device, dtype=torch.float32)
+    return torch.full((1,), float(v), dtype=torch.float32, device=device)
+
+
+def _rocm_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("admmtor (MI355X build): fft_admm_tv runs its HIP kernels on a ROCm device and none "
+                           "is visible. There is no CPU path.")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _stage(xin, lmbd, rho, kern):
+    """Host inputs -> the current ROCm device (the reference accepts CPU tensors, e.g.
+    test_torch_admm.ipynb:249,302).  The copies are differentiable ``.to()`` calls, so gradients
+    flow back to host tensors / parameters.  Device inputs pass through unchanged."""
+    if xin.device.type in ("cuda", "meta"):  # meta: shape inference through the ops' fake kernels
+        return xin, lmbd, rho, kern
+    dev = _rocm_device()
+    mv = (lambda v: v.to(dev) if isinstance(v, torch.Tensor) else v)
+    return xin.to(dev), mv(lmbd), mv(rho), kern.to(dev)
+
+
 def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.Tensor, iso: bool, maxit: int,
            hook=None):
     """Run the HIP solver: x32 (B,C,H,W) fp32 contiguous on the device -> new tensor.
+    Without a hook this is the dispatcher op admm_hip::fft_admm_tv_fwd (admmtor._ops).
     `hook`: an _native.AllReduceHook for iso over a batch sharded across ranks; its callback is
     bound to this call's workspace only (no process-global state)."""
+    if hook is None or not iso:
+        return torch.ops.admm_hip.fft_admm_tv_fwd(x32, lam, rho, k32, bool(iso), int(maxit))
     lib = _native.load()
     B, C, H, W = x32.shape
     G = lam.numel()  # modules solved together (fft_admm_tv_grouped); 1 for fft_admm_tv
     k = int(k32.shape[-1]) if k32.numel() > 0 else 0
-    bound = hook.bind() if (hook is not None and iso) else None
+    bound = hook.bind()
     d = _native.desc(B, C, H, W, k, iso, maxit, 0, G, bound)
     if not _native.supported(H, W):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} outside [1, 4096]")
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
-    if bound is not None:
-        bound.add(ws)
+    bound.add(ws)
     out = torch.empty((G * B, C, H, W), dtype=torch.float32, device=x32.device)
     stream = torch.cuda.current_stream(x32.device).cuda_stream
     _native.check(lib.admm_tv_forward(
         d, x32.data_ptr(), k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(),
         out.data_ptr(), ws.data_ptr(), ws.numel(), stream))
-    if bound is not None:
-        bound.check()
+    bound.check()
     return out
 
 
@@ -145,8 +171,12 @@ def fft_admm_tv(xin: torch.Tensor,
     forward differences, ``H_t`` = centred circular convolution with ``kern``,
     soft (``iso=False``) or batch/channel-coupled block (``iso=True``)
     shrinkage, ``tau = lmbd / rho``, ``maxit`` iterations from zero, returns the
-    last x with xin's shape.  Runs on ROCm tensors only (fp32; bf16/fp16 under
-    ``torch.autocast`` compute in fp32 and return fp32, as the reference does).
+    last x with xin's shape, on xin's device.  The solve always runs as HIP kernels on a ROCm
+    device: host tensors are staged to the current device and the result copied back
+    (autograd flows through both copies).  Arithmetic is fp32: fp32 inputs return fp32, fp64
+    inputs return fp64 (computed in fp32, within 1e-5 relative L2 of the reference's fp64
+    result), bf16/fp16 under ``torch.autocast`` compute in fp32 and return fp32, as the
+    reference does.
     """
     return _fft_admm_tv_impl(xin, lmbd, rho, kern, iso, maxit)
 
@@ -156,28 +186,36 @@ def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> 
     if not isinstance(kern, torch.Tensor):
         kern = torch.as_tensor(kern)
     _check_inputs(xin, kern)
-    if not xin.is_cuda:
-        raise RuntimeError("admmtor (MI355X build): fft_admm_tv runs on ROCm device tensors only; "
-                           "move xin (and kern) to the GPU. There is no CPU path.")
+    home, out_dtype = xin.device, (torch.float64 if xin.dtype == torch.float64 else torch.float32)
     maxit = max(0, int(maxit))  # the reference loops over torch.arange(0, maxit): negative -> no iteration
     # empty batch: the reference's ops return an empty result of the same shape.  An empty shard of
     # an iso solve over ranks still runs: it must take part in every iteration's all-reduce.
     shard_member = hook is not None and iso and xin.shape[2] > 0 and xin.shape[3] > 0
     if xin.numel() == 0 and not shard_member:
-        return torch.zeros(xin.shape, dtype=torch.float32, device=xin.device)
+        return torch.zeros(xin.shape, dtype=out_dtype, device=home)
+    xin, lmbd, rho, kern = _stage(xin, lmbd, rho, kern)
     dev = xin.device
-    x32 = xin.detach().to(torch.float32).contiguous()
-    k32 = kern.detach().to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \
-        torch.empty(0, dtype=torch.float32, device=dev)
-    lam = _as_device_scalar(lmbd, dev)
-    rh = _as_device_scalar(rho, dev)
     needs_grad = torch.is_grad_enabled() and (
         xin.requires_grad or (isinstance(lmbd, torch.Tensor) and lmbd.requires_grad)
         or (isinstance(rho, torch.Tensor) and rho.requires_grad) or kern.requires_grad)
     if needs_grad:
-        from .._backward import fft_admm_tv_autograd
-        return fft_admm_tv_autograd(xin, lmbd, rho, kern, bool(iso), maxit, hook=hook)
-    return _solve(x32, k32, lam, rh, bool(iso), maxit, hook=hook)
+        if hook is not None and iso:
+            from .._backward import fft_admm_tv_autograd
+            out = fft_admm_tv_autograd(xin, lmbd, rho, kern, bool(iso), maxit, hook=hook)
+        else:
+            x32 = xin.to(torch.float32).contiguous()  # differentiable cast (fp64 / autocast half inputs)
+            k32 = kern.to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \
+                torch.empty(0, dtype=torch.float32, device=dev)
+            psf_grad = kern.requires_grad and kern.numel() > 0
+            out, _ = torch.ops.admm_hip.fft_admm_tv_fwd_train(
+                x32, _scalar_input(lmbd, dev), _scalar_input(rho, dev), k32, bool(iso), maxit, psf_grad)
+    else:
+        x32 = xin.detach().to(torch.float32).contiguous()
+        k32 = kern.detach().to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \
+            torch.empty(0, dtype=torch.float32, device=dev)
+        out = _solve(x32, k32, _as_device_scalar(lmbd, dev), _as_device_scalar(rho, dev), bool(iso), maxit,
+                     hook=hook)
+    return out.to(device=home, dtype=out_dtype)
 
 
 def fft_admm_tv_grouped(xin: torch.Tensor, lmbds, rhos, kern: torch.Tensor, iso: bool = False,
@@ -208,8 +246,13 @@ def fft_admm_tv_grouped(xin: torch.Tensor, lmbds, rhos, kern: torch.Tensor, iso:
     needs_grad = torch.is_grad_enabled() and (
         xin.requires_grad or any(isinstance(v, torch.Tensor) and v.requires_grad for v in (*lmbds, *rhos)))
     if needs_grad:
-        from .._backward import fft_admm_tv_grouped_autograd
-        out = fft_admm_tv_grouped_autograd(xin, lmbds, rhos, kern, bool(iso), maxit)
+        # lambda and rho stacked into (G,) tensors differentiably, so each module's parameters get theirs
+        x32 = xin.to(torch.float32).contiguous()
+        k32 = kern.detach().to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \
+            torch.empty(0, dtype=torch.float32, device=dev)
+        lam_t = torch.cat([_scalar_input(v, dev) for v in lmbds])
+        rho_t = torch.cat([_scalar_input(v, dev) for v in rhos])
+        out, _ = torch.ops.admm_hip.fft_admm_tv_fwd_train(x32, lam_t, rho_t, k32, bool(iso), maxit, False)
     else:
         x32 = xin.detach().to(torch.float32).contiguous()
         k32 = kern.detach().to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \

@@ -101,12 +101,17 @@ def sharded_fft_admm_tv(x_local: torch.Tensor, lmbd, rho, kern: torch.Tensor, is
         dist.all_reduce(n, group=group)
         B = int(n.item())
     per = -(-B // world)
-    pad = torch.zeros((per,) + tuple(out.shape[1:]), dtype=out.dtype, device=out.device)
-    pad[: out.shape[0]] = out
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(bufs, pad, group=group)
-    parts = []
-    for r in range(world):
-        s, e = shard_bounds(B, world, r)
-        parts.append(bufs[r][: e - s])
-    return torch.cat(parts, 0)
+    if out.shape[0] == per:
+        src = out.contiguous()
+    else:  # a short shard (B not divisible by the world size) is padded to the common size
+        src = torch.zeros((per,) + tuple(out.shape[1:]), dtype=out.dtype, device=out.device)
+        src[: out.shape[0]] = out
+    full = torch.empty((world * per,) + tuple(out.shape[1:]), dtype=out.dtype, device=out.device)
+    if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo":
+        dist.all_gather_into_tensor(full, src, group=group)  # one RCCL collective, no staging copies
+    else:
+        dist.all_gather(list(full.chunk(world, 0)), src, group=group)
+    if per * world == B:  # equal shards: the gathered buffer is the output
+        return full
+    return torch.cat([full[r * per: r * per + (shard_bounds(B, world, r)[1] - shard_bounds(B, world, r)[0])]
+                      for r in range(world)], 0)
