@@ -61,6 +61,10 @@ def test_g7_odd_size_vs_reference(cuda_dev):
     ((1, 2, 97, 101), ("gauss:2", 7), False, 20),          # prime sizes (generic radix stages)
     ((1, 1, 360, 1000), ("motion", 15), False, 10),        # 2^3 3^2 5 x 2^3 5^3
     ((1, 1, 64, 4096), ("gauss:2", 11), False, 5),         # W beyond the fast path
+    ((1, 1, 143, 121), ("gauss:1.5", 7), True, 15),        # 11*13 x 11^2: two Bluestein stages each
+    ((1, 1, 509, 37), ("motion", 9), False, 10),           # prime 509: Bluestein at M = 1024
+    ((1, 2, 26, 1021), None, False, 8),                    # prime 1021 > 512: the direct prime stage
+    ((1, 1, 214, 321), ("gauss:2", 7), True, 12),          # 2*107 x 3*107
 ])
 def test_generic_shapes_vs_oracle(cuda_dev, shape, psf, iso, it):
     from admmtor.synth import blurred_batch, make_psf
@@ -71,6 +75,25 @@ def test_generic_shapes_vs_oracle(cuda_dev, shape, psf, iso, it):
     err = rel(got, ref)
     print(shape, psf, "iso" if iso else "aniso", "rel vs fp64 oracle:", err)
     assert err <= TOL_REF64
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 321, 481), (1, 2, 143, 509), (1, 1, 37, 74)])
+def test_bluestein_matches_direct_prime_stages(cuda_dev, shape, monkeypatch):
+    """Chirp-z (Bluestein) stages vs the O(R)-per-output prime stages (ADMM_BLUE_MIN=0): both are
+    fp32 evaluations of the same transform; Bluestein must meet the fp64-oracle gate and be no less
+    accurate than the direct stages (within 2x + 1e-6; the direct O(R) stage itself drifts to ~1e-5
+    for R = 509)."""
+    from admmtor.synth import blurred_batch, make_psf
+    k = make_psf("gauss:1.5", 9)
+    x = blurred_batch(*shape, k, seed=7)
+    ref = oracle(x, k, 0.01, 0.02, False, 15)
+    monkeypatch.setenv("ADMM_BLUE_MIN", "0")
+    e_direct = rel(solve(x, k, 0.01, 0.02, False, 15, cuda_dev), ref)
+    monkeypatch.setenv("ADMM_BLUE_MIN", "11")
+    e_blue = rel(solve(x, k, 0.01, 0.02, False, 15, cuda_dev), ref)
+    print(shape, f"vs fp64 oracle: bluestein {e_blue:.3e}, direct {e_direct:.3e}")
+    assert e_blue <= TOL_REF64
+    assert e_blue <= 2 * e_direct + 1e-6
 
 
 def test_generic_psf_transpose(cuda_dev):

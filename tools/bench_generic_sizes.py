@@ -1,0 +1,58 @@
+"""Per-pixel cost of the generic (non-power-of-two) path across image sizes, vs the fused path.
+
+  python tools/bench_generic_sizes.py [NAME=v1,v2 ...]   (env knobs, swept in-process per shape)
+Prints per shape (and knob value): iterations/s and ns per iteration per megapixel.
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "torch-admm-deconv_amd"))
+import torch  # noqa: E402
+
+from admmtor.eops.deconv import fft_admm_tv  # noqa: E402
+from admmtor.synth import blurred_batch, make_psf  # noqa: E402
+
+SHAPES = [  # B, C, H, W
+    (32, 3, 321, 481),    # BSD (3*107, 13*37)
+    (32, 3, 480, 640),    # VGA (2^5*3*5, 2^7*5)
+    (8, 3, 1080, 1920),   # HD (2^3*3^3*5, 2^7*3*5)
+    (16, 3, 500, 500),    # 2^2*5^3
+    (16, 3, 509, 509),    # prime
+    (32, 3, 512, 512),    # fused reference point (C2 shape)
+]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    psf = make_psf("gauss:1.5", 9).to(dev)
+    maxit = 20
+    knobs = [a.split("=") for a in sys.argv[1:]]
+    settings = [[]]
+    for name, vals in knobs:
+        settings = [st + [(name, v)] for st in settings for v in vals.split(",")]
+    shapes = SHAPES
+    if os.environ.get("SHAPES"):  # e.g. SHAPES=0,4 (indices into SHAPES)
+        shapes = [SHAPES[int(i)] for i in os.environ["SHAPES"].split(",")]
+    for B, C, H, W in shapes:
+        x = blurred_batch(B, C, H, W, psf.cpu(), seed=1, device=dev)
+        for st in settings:
+            for name, v in st:
+                os.environ[name] = v
+            fft_admm_tv(x, 0.01, 0.02, psf, False, maxit)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n = 3
+            for _ in range(n):
+                fft_admm_tv(x, 0.01, 0.02, psf, False, maxit)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / n / maxit
+            mpx = B * C * H * W / 1e6
+            tag = " ".join(f"{k}={v}" for k, v in st)
+            print(f"{B}x{C}x{H}x{W} {tag}: {1 / dt:8.1f} it/s  {dt * 1e3:7.3f} ms/it  {dt * 1e9 / mpx:8.1f} ns/it/Mpx",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

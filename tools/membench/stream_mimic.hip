@@ -335,10 +335,7 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
     const unsigned x = b & 7u, i = b >> 3, q = nb >> 3, r = nb & 7u;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
-#ifndef SO_NT
-#define SO_NT true
-#endif
-template <int R, int T>
+template <int R, int T, bool SO_NT = true, bool IN_T = false>
 __global__ void __launch_bounds__(256) k_mimic_ot(const cf* __restrict__ sp, const cf* __restrict__ uxi,
                                                   const cf* __restrict__ uyi, const cf* __restrict__ b,
                                                   cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
@@ -351,13 +348,16 @@ __global__ void __launch_bounds__(256) k_mimic_ot(const cf* __restrict__ sp, con
     const int i0 = (int)(strip % spp) * R;
     const size_t base = (size_t)p * H * N;
     cf acc[E];
-    for (int j = 0; j < E; ++j) acc[j] = ld(&sp[base + (size_t)((i0 - 1 + H) & (H - 1)) * N + t + L * j], true);
+    {
+        const int gp = (i0 - 1 + H) & (H - 1);
+        for (int j = 0; j < E; ++j) acc[j] = ld(&sp[base + (IN_T ? toff<T>(gp, t + L * j) : (size_t)gp * N + t + L * j)], !IN_T);
+    }
     for (int rr = 0; rr <= R; ++rr) {
         const int gi = (i0 + rr) & (H - 1), gm = (i0 + rr - 1 + H) & (H - 1);
         const size_t ro = base + (size_t)gi * N;
         const size_t rm = base + (size_t)gm * N;
         cf x[E], uy[E];
-        for (int j = 0; j < E; ++j) x[j] = ld(&sp[ro + t + L * j], true);
+        for (int j = 0; j < E; ++j) x[j] = ld(&sp[base + (IN_T ? toff<T>(gi, t + L * j) : (size_t)gi * N + t + L * j)], !IN_T);
         for (int j = 0; j < E; ++j) { uy[j] = ld(&uyi[ro + t + L * j], true); uy[j].x += x[j].x; uy[j].y += acc[j].y; }
         if (rr < R) for (int j = 0; j < E; ++j) st(&uyo[ro + t + L * j], uy[j], true);
         if (rr >= 1) {
@@ -418,6 +418,25 @@ int main() {
         printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
     const double arr = (double)n * sizeof(cf);
+    if (getenv("MIXED_SWEEP2")) {
+        const long long ns = (long long)P * H / 8;
+        const int colblocks = N / 8;
+        for (int rep = 0; rep < 3; ++rep) {
+            timeit("A row-major nt (prod) R=8", 7 * arr, [&] { k_mimic<8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A out-tiled T=8 plain st", 7 * arr, [&] { k_mimic_ot<8, 8, false><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A in+out tiled T=8 nt st", 7 * arr, [&] { k_mimic_ot<8, 8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A in+out tiled T=8 plain st", 7 * arr, [&] { k_mimic_ot<8, 8, false, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A in-tiled T=8 only", 7 * arr, [&] { k_mimic_ot<8, 8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("B row->row remap in place", 2 * arr, [&] { k_colmimic_mix<512, 8, false, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[0], buf[0], H, colblocks); });
+            timeit("B row->row remap oop", 2 * arr, [&] { k_colmimic_mix<512, 8, false, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+            timeit("B row->row noremap in place", 2 * arr, [&] { k_colmimic_mix<512, 8, false, false, false><<<(unsigned)(P * colblocks), 512>>>(buf[0], buf[0], H, colblocks); });
+            timeit("B tiled->tiled remap in place", 2 * arr, [&] { k_colmimic_mix<512, 8, true, true, true><<<(unsigned)(P * colblocks), 512>>>(buf[0], buf[0], H, colblocks); });
+            timeit("B C=16 1024thr row in place", 2 * arr, [&] { k_colmimic<16, 1024><<<(unsigned)(P * colblocks / 2), 1024>>>(buf[0], H, colblocks / 2); });
+            timeit("copy float4", 2 * arr, [&] { k_copy<false><<<16384, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
+            timeit("copy float2 1/thread nt", 2 * arr, [&] { k_copy2<true><<<(unsigned)(n / 256), 256>>>((const float2*)buf[0], (float2*)buf[1]); });
+        }
+        return 0;
+    }
     if (getenv("MIXED_SWEEP")) {
         const long long ns = (long long)P * H / 8;
         const int colblocks = N / 8;

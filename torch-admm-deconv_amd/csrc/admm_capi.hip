@@ -101,6 +101,8 @@ int env_int(const char* name, int dflt) {
     return s ? std::atoi(s) : dflt;
 }
 
+GPlan make_plan(int n);  // generic-size transform plan (below)
+
 // modules solved together (admm_tv_desc.groups)
 int ngroups_of(const admm_tv_desc& d) { return d.groups > 1 ? d.groups : 1; }
 
@@ -135,8 +137,9 @@ Layout make_layout(const admm_tv_desc& d) {
     L.b = k > 0 ? take(img_m) : 0;  // b = H_t(xin) is shared by the modules
     L.fcT = take(G * (N + 1) * H * sizeof(float));  // one Wiener factor per module (its rho)
     L.mT = take((N + 1) * H * sizeof(cf));
-    L.twW = take(W * sizeof(cf));
-    L.twH = take(H * sizeof(cf));
+    // twiddles; on the generic path followed by the plan's Bluestein tables (make_plan)
+    L.twW = take((W + (L.gen ? make_plan((int)W).ntab : 0)) * sizeof(cf));
+    L.twH = take((H + (L.gen ? make_plan((int)H).ntab : 0)) * sizeof(cf));
     L.twHd = take(H * sizeof(double2));
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
@@ -406,6 +409,15 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
     hipLaunchKernelGGL(k_tables, dim3((std::max(H, W) + nt - 1) / nt), dim3(nt), 0, s, at<cf>(ws, Lo.twW),
                        at<cf>(ws, Lo.twH), at<double2>(ws, Lo.twHd), H, W);
     if (int e = launch_check("k_tables")) return e;
+    if (Lo.gen) {  // Bluestein tables of the row and column plans, after their twiddles
+        for (int dim = 0; dim < 2; ++dim) {
+            const GPlan pl = make_plan(dim == 0 ? W : H);
+            if (pl.ntab == 0) continue;
+            hipLaunchKernelGGL(k_blue_tables, dim3((3 * 1024 + nt - 1) / nt), dim3(nt), 0, s,
+                               at<cf>(ws, dim == 0 ? Lo.twW : Lo.twH), pl);
+            if (int e = launch_check("k_blue_tables")) return e;
+        }
+    }
     if (k > 0) {
         const int n = k * (N + 1);
         hipLaunchKernelGGL(k_psf_rows, dim3((n + nt - 1) / nt), dim3(nt), 0, s, kern, at<double2>(ws, Lo.G), k, N, W);
@@ -464,7 +476,53 @@ int psf_transpose_into(const admm_tv_desc& d, const Layout& Lo, void* ws, const 
 
 
 // ------------------------------------------------------------------ generic sizes (generic_kernels.hpp)
+GPlan make_plan_radices(int n);
+
+// Bluestein stages (generic_kernels.hpp gstage_blue): a prime radix R >= ADMM_BLUE_MIN (default
+// below) with 2R - 1 <= 1024 runs as a chirp-z transform on the register-resident power-of-two FFT;
+// larger primes keep the O(R)-per-output stage.  ADMM_BLUE_MIN <= 0 disables it (A/B).
+int blue_min() { return env_int("ADMM_BLUE_MIN", 41); }
+
 GPlan make_plan(int n) {
+    GPlan p = make_plan_radices(n);
+    const int bmin = blue_min();
+    int M = 0;  // one Bluestein size for the plan: M = 2^k >= 2R - 1 for its largest such prime
+    for (int s = 0; s < p.nst; ++s) {
+        const int R = p.rad[s];
+        if (bmin <= 0 || R <= 7 || R < bmin || 2 * R - 1 > 1024) continue;
+        int m = 32;
+        while (m < 2 * R - 1) m *= 2;
+        M = std::max(M, m);
+    }
+    int off = n;
+    for (int s = 0; s < p.nst; ++s) {
+        const int R = p.rad[s];
+        const bool blue = M > 0 && R > 7 && R >= bmin && 2 * R - 1 <= 1024;
+        p.bst[s] = blue ? M : 0;
+        p.boff[s] = blue ? off : 0;
+        if (blue) off += R + 2 * M;
+    }
+    p.bm = M;
+    p.ntab = off - n;
+    p.xslots = M > 0 ? (256 / (M / blue_e(M))) * (M + M / 8) : 0;
+    return p;
+}
+
+// the kernel instantiation for a plan's Bluestein size
+template <class F> int with_bm(int bm, F&& f) {
+    switch (bm) {
+        case 0: return f(std::integral_constant<int, 0>{});
+        case 32: return f(std::integral_constant<int, 32>{});
+        case 64: return f(std::integral_constant<int, 64>{});
+        case 128: return f(std::integral_constant<int, 128>{});
+        case 256: return f(std::integral_constant<int, 256>{});
+        case 512: return f(std::integral_constant<int, 512>{});
+        case 1024: return f(std::integral_constant<int, 1024>{});
+        default: return fail(ADMM_TV_EUNSUPPORTED, "generic plan: Bluestein size");
+    }
+}
+
+GPlan make_plan_radices(int n) {
     GPlan p{};
     p.n = n;
     int m = n;
@@ -516,44 +574,45 @@ int gcol_cols(int H) {
 
 int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hipStream_t s) {
     GRowArgs a{img, spec, nullptr, tw, make_plan(W), rows, grow_lines(W)};
-    const size_t lds = sizeof(cf) * (size_t)W * (1 + 2 * a.lines);
-    if (int e = set_lds(k_grow_fwd, lds)) return e;
-    hipLaunchKernelGGL(k_grow_fwd, dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
-    return launch_check("k_grow_fwd");
+    const size_t lds = sizeof(cf) * ((size_t)W * (1 + 2 * a.lines) + a.plan.ntab + a.plan.xslots);
+    return with_bm(a.plan.bm, [&](auto bm) {
+        constexpr int BM = decltype(bm)::value;
+        if (int e = set_lds(k_grow_fwd<BM>, lds)) return e;
+        hipLaunchKernelGGL(k_grow_fwd<BM>, dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
+        return launch_check("k_grow_fwd");
+    });
 }
 int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hipStream_t s) {
     GRowArgs a{nullptr, const_cast<cf*>(spec), img, tw, make_plan(W), rows, grow_lines(W)};
-    const size_t lds = sizeof(cf) * (size_t)W * (1 + 2 * a.lines);
-    if (int e = set_lds(k_grow_inv, lds)) return e;
-    hipLaunchKernelGGL(k_grow_inv, dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
-    return launch_check("k_grow_inv");
+    const size_t lds = sizeof(cf) * ((size_t)W * (1 + 2 * a.lines) + a.plan.ntab + a.plan.xslots);
+    return with_bm(a.plan.bm, [&](auto bm) {
+        constexpr int BM = decltype(bm)::value;
+        if (int e = set_lds(k_grow_inv<BM>, lds)) return e;
+        hipLaunchKernelGGL(k_grow_inv<BM>, dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
+        return launch_check("k_grow_inv");
+    });
+}
+template <int MODE, int BM> int gcol_launch(const GColArgs& a, size_t lds, dim3 grid, hipStream_t s) {
+    if (int e = set_lds(k_gcol<MODE, BM>, lds)) return e;
+    hipLaunchKernelGGL((k_gcol<MODE, BM>), grid, dim3(256), lds, s, a);
+    return launch_check("k_gcol");
 }
 int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H, int W, long long P, int mode,
          hipStream_t s) {
     const int Wh = W / 2 + 1, cols = gcol_cols(H);
     const int colblocks = (Wh + cols - 1) / cols;
     GColArgs a{spec, dump, fcT, mT, tw, make_plan(H), Wh, cols, colblocks, P};
-    const size_t lds = sizeof(cf) * (size_t)H * (1 + 2 * cols);
+    const size_t lds = sizeof(cf) * ((size_t)H * (1 + 2 * cols) + a.plan.ntab + a.plan.xslots);
     const dim3 grid((unsigned)(P * colblocks));
-    switch (mode) {
-        case 0:
-            if (int e = set_lds(k_gcol<0>, lds)) return e;
-            hipLaunchKernelGGL(k_gcol<0>, grid, dim3(256), lds, s, a);
-            break;
-        case 1:
-            if (int e = set_lds(k_gcol<1>, lds)) return e;
-            hipLaunchKernelGGL(k_gcol<1>, grid, dim3(256), lds, s, a);
-            break;
-        case 2:
-            if (int e = set_lds(k_gcol<2>, lds)) return e;
-            hipLaunchKernelGGL(k_gcol<2>, grid, dim3(256), lds, s, a);
-            break;
-        default:
-            if (int e = set_lds(k_gcol<3>, lds)) return e;
-            hipLaunchKernelGGL(k_gcol<3>, grid, dim3(256), lds, s, a);
-            break;
-    }
-    return launch_check("k_gcol");
+    return with_bm(a.plan.bm, [&](auto bm) {
+        constexpr int BM = decltype(bm)::value;
+        switch (mode) {
+            case 0: return gcol_launch<0, BM>(a, lds, grid, s);
+            case 1: return gcol_launch<1, BM>(a, lds, grid, s);
+            case 2: return gcol_launch<2, BM>(a, lds, grid, s);
+            default: return gcol_launch<3, BM>(a, lds, grid, s);
+        }
+    });
 }
 // img_out = real part of the 2-D transform chain  rowFFT -> column pass (mode) -> rowIFFT  of img_in
 int gapply(const float* img_in, float* img_out, cf* spec, const Layout& Lo, void* ws, const admm_tv_desc& d, int mode,

@@ -23,10 +23,24 @@ namespace admm {
 
 constexpr int GMAXST = 24;  // max number of radix stages (n <= 8192 -> at most 13 factors)
 
+// A stage whose radix is a prime R > 7 runs either as the O(R)-per-output stage (gstage_any) or,
+// for R >= the Bluestein threshold (admm_capi.hip make_plan), as a chirp-z transform: the R-point
+// DFT as a length-M circular convolution (M = 2^k >= 2R - 1) done with the register-resident
+// power-of-two FFT of fft_core.hpp (gstage_blue).  Its tables follow the n twiddles of `tw`:
+// chirp c_q = exp(-i pi q^2 / R) (R values), B = FFT_M(conj c, even-extended) / M (M values),
+// and the M-point twiddles exp(-2 pi i j / M) (M values).
 struct GPlan {
     int n, nst;
     int rad[GMAXST];
+    int bst[GMAXST];   // Bluestein size M of stage s (0: direct stage)
+    int boff[GMAXST];  // offset (complex values) of stage s's tables from the start of tw
+    int ntab;          // table entries after the n twiddles
+    int xslots;        // exchange slots (complex values) the Bluestein stages need
+    int bm;            // the plan's Bluestein size M (all its Bluestein stages), 0: none
 };
+
+// values per lane of the power-of-two transform of length M (fft_core.hpp RowCfg)
+__host__ __device__ constexpr int blue_e(int M) { return M <= 32 ? 4 : M <= 512 ? 8 : 16; }
 
 // ---------------------------------------------------------------------------
 // one Stockham stage over `lines` transforms of length n held in LDS as [i][lines]
@@ -177,21 +191,80 @@ __device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict_
     }
 }
 
-// full transform; data starts in bufA, returns the buffer holding the result
-template <int DIR>
-__device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf* __restrict__ tw) {  // bufA is clobbered
+// Bluestein stage (radix R prime, M = 2^k >= 2R - 1): every butterfly (vt, line) is one item,
+// run by a sub-group of L = M / E lanes holding its length-M sequence in registers:
+//   a_q = x_q W_{NS R}^{m q} c_q (q < R, else 0);  A = FFT_M(a);  A *= B;  a = IFFT_M(A);
+//   X_k = c_k a_k  (k < R)  -- with conj(c), conj(B) for the inverse direction.
+// The exchange area holds one RowBuf per sub-group; all sub-groups run the same number of
+// rounds, so the wave-level exchange of fft() never diverges (idle items are masked).
+template <int DIR, int M>
+__device__ __forceinline__ void gstage_blue(const cf* __restrict__ src, cf* __restrict__ dst, int n, int NS, int R,
+                                            int lines, const cf* __restrict__ tw, const cf* __restrict__ bt,
+                                            cf* __restrict__ xbuf) {
+    constexpr int E = RowCfg<M>::E, L = M / E;
+    static_assert(L <= 64, "one Bluestein sequence per sub-group inside one wave");
+    const int nsg = blockDim.x / L;
+    const int sg = threadIdx.x / L, t = threadIdx.x % L;
+    const RowBuf buf{xbuf + sg * RowBuf::slots(M)};
+    const cf* chirp = bt;
+    const cf* Bf = bt + R;
+    const cf* twM = bt + R + M;
+    const int nb = n / R, span = NS * R, tstride = n / span;
+    const int items = nb * lines;
+    const int rounds = (items + nsg - 1) / nsg;
+    for (int rr = 0; rr < rounds; ++rr) {
+        const int item = rr * nsg + sg;
+        const bool live = item < items;
+        const int c = live ? item % lines : 0, vt = live ? item / lines : 0;
+        const int m = vt % NS;
+        cf v[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const int q = t + L * j;
+            cf x = mkc(0.f, 0.f);
+            if (live && q < R) {
+                x = src[(vt + q * nb) * lines + c];
+                if (q > 0 && m > 0) x = cmul(x, twid<DIR>(tw, ((m * q) % span) * tstride));
+                x = DIR < 0 ? cmul(x, chirp[q]) : cmulc(x, chirp[q]);
+            }
+            v[j] = x;
+        }
+        fft<M, L, -1, 0, 1>(v, buf, twM, t);
+#pragma unroll
+        for (int j = 0; j < E; ++j) v[j] = DIR < 0 ? cmul(v[j], Bf[t + L * j]) : cmulc(v[j], Bf[t + L * j]);
+        fft<M, L, +1, 0, 1>(v, buf, twM, t);
+        cf* out = dst + ((size_t)(vt / NS) * span + m) * lines + c;
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const int k = t + L * j;
+            if (live && k < R) out[(size_t)k * NS * lines] = DIR < 0 ? cmul(v[j], chirp[k]) : cmulc(v[j], chirp[k]);
+        }
+    }
+}
+
+// full transform; data starts in bufA, returns the buffer holding the result.  tw: the n
+// twiddles followed by the plan's Bluestein tables (LDS); xbuf: pl.xslots exchange slots.
+// BM: the plan's Bluestein size (a template parameter, so a kernel without Bluestein stages keeps
+// its small register footprint; each BM is its own kernel instantiation).
+template <int DIR, int BM>
+__device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf* __restrict__ tw,
+                        cf* __restrict__ xbuf) {  // bufA is clobbered
     cf* src = bufA;
     cf* dst = bufB;
     int NS = 1;
     for (int s = 0; s < pl.nst; ++s) {
         const int R = pl.rad[s];
-        switch (R) {
-            case 2: gstage_r<DIR, 2>(src, dst, pl.n, NS, lines, tw); break;
-            case 3: gstage_r<DIR, 3>(src, dst, pl.n, NS, lines, tw); break;
-            case 4: gstage_r<DIR, 4>(src, dst, pl.n, NS, lines, tw); break;
-            case 5: gstage_r<DIR, 5>(src, dst, pl.n, NS, lines, tw); break;
-            case 7: gstage_r<DIR, 7>(src, dst, pl.n, NS, lines, tw); break;
-            default: gstage_any<DIR>(src, dst, pl.n, NS, R, lines, tw); break;
+        if (BM > 0 && pl.bst[s] > 0) {
+            if constexpr (BM > 0) gstage_blue<DIR, BM>(src, dst, pl.n, NS, R, lines, tw, tw + pl.boff[s], xbuf);
+        } else {
+            switch (R) {
+                case 2: gstage_r<DIR, 2>(src, dst, pl.n, NS, lines, tw); break;
+                case 3: gstage_r<DIR, 3>(src, dst, pl.n, NS, lines, tw); break;
+                case 4: gstage_r<DIR, 4>(src, dst, pl.n, NS, lines, tw); break;
+                case 5: gstage_r<DIR, 5>(src, dst, pl.n, NS, lines, tw); break;
+                case 7: gstage_r<DIR, 7>(src, dst, pl.n, NS, lines, tw); break;
+                default: gstage_any<DIR>(src, dst, pl.n, NS, R, lines, tw); break;
+            }
         }
         __syncthreads();
         cf* t = src;
@@ -200,6 +273,42 @@ __device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf
         NS *= R;
     }
     return src;
+}
+
+// Bluestein tables of a plan, written after the n twiddles of `tab` (fp64 arithmetic, fp32 store):
+// per Bluestein stage s (R = rad[s], M = bst[s]) at tab + boff[s]: chirp[R], B[M], twM[M].
+__global__ void k_blue_tables(cf* __restrict__ tab, GPlan pl) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int s = 0; s < pl.nst; ++s) {
+        const int R = pl.rad[s], M = pl.bst[s];
+        if (M == 0 || i >= R + 2 * M) continue;
+        cf* o = tab + pl.boff[s];
+        double re, im;
+        if (i < R) {  // c_q = exp(-i pi q^2 / R)
+            const long long q2 = ((long long)i * i) % (2LL * R);
+            sincospi((double)q2 / R, &im, &re);
+            o[i] = mkc((float)re, (float)-im);
+        } else if (i < R + M) {  // B[k] = (1/M) sum_j bt_j exp(-2 pi i j k / M), bt = conj(c) even-extended
+            const int k = i - R;
+            double sr = 0.0, si = 0.0;
+            for (int j = 0; j < M; ++j) {
+                const int jj = j < R ? j : (M - j < R ? M - j : -1);
+                if (jj < 0) continue;
+                const long long q2 = ((long long)jj * jj) % (2LL * R);
+                double bs, bc;
+                sincospi((double)q2 / R, &bs, &bc);  // bt_j = exp(+i pi jj^2 / R)
+                double ws, wc;
+                sincospi(2.0 * (double)(((long long)j * k) % M) / M, &ws, &wc);  // exp(-i ...) = wc - i ws
+                sr += bc * wc + bs * ws;
+                si += bs * wc - bc * ws;
+            }
+            o[i] = mkc((float)(sr / M), (float)(si / M));
+        } else {  // twM[j] = exp(-2 pi i j / M)
+            const int j = i - R - M;
+            sincospi(2.0 * (double)j / M, &im, &re);
+            o[i] = mkc((float)re, (float)-im);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -218,13 +327,15 @@ struct GRowArgs {
 // Real rows are transformed two at a time: rows a, b as one complex row z = a + i b, whose
 // spectrum Z gives A[k] = (Z[k] + conj Z[-k]) / 2 and B[k] = (Z[k] - conj Z[-k]) / 2i.  A block
 // holds `lines` complex rows = 2 * lines real rows.
+template <int BM>
 __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     cf* tw = reinterpret_cast<cf*>(smem);
-    cf* A = tw + W;
+    cf* A = tw + W + a.plan.ntab;
     cf* B = A + (size_t)W * lines;
-    for (int i = threadIdx.x; i < W; i += blockDim.x) tw[i] = a.tw[i];
+    cf* X = B + (size_t)W * lines;  // Bluestein exchange slots
+    for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) tw[i] = a.tw[i];
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);  // real rows in this block
     for (int idx = threadIdx.x; idx < W * 2 * lines; idx += blockDim.x) {
@@ -234,7 +345,7 @@ __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
         slot[rr & 1] = v;  // even row -> real part, odd row -> imaginary part
     }
     __syncthreads();
-    const cf* res = gfft_lds<-1>(A, B, a.plan, lines, tw);
+    const cf* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
     for (int idx = threadIdx.x; idx < Wh * lines; idx += blockDim.x) {
         const int c = idx / Wh, k = idx % Wh;
         const cf z = res[k * lines + c];
@@ -245,13 +356,15 @@ __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
     }
 }
 
+template <int BM>
 __global__ void __launch_bounds__(256) k_grow_inv(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     cf* tw = reinterpret_cast<cf*>(smem);
-    cf* A = tw + W;
+    cf* A = tw + W + a.plan.ntab;
     cf* B = A + (size_t)W * lines;
-    for (int i = threadIdx.x; i < W; i += blockDim.x) tw[i] = a.tw[i];
+    cf* X = B + (size_t)W * lines;
+    for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) tw[i] = a.tw[i];
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);
     // Hermitian completion of a half spectrum: X[k] = conj X[W - k] for k >= Wh; the imaginary
@@ -272,7 +385,7 @@ __global__ void __launch_bounds__(256) k_grow_inv(GRowArgs a) {
         A[k * lines + c] = mkc(xa.x - xb.y, xa.y + xb.x);  // Z = Xa + i Xb
     }
     __syncthreads();
-    const cf* res = gfft_lds<+1>(A, B, a.plan, lines, tw);
+    const cf* res = gfft_lds<+1, BM>(A, B, a.plan, lines, tw, X);
     for (int idx = threadIdx.x; idx < W * 2 * lines; idx += blockDim.x) {
         const int rr = idx / W, i = idx % W;
         if (rr < nl) {
@@ -301,14 +414,15 @@ struct GColArgs {
     long long P;
 };
 
-template <int MODE>
+template <int MODE, int BM>
 __global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
     cf* tw = reinterpret_cast<cf*>(smem);
-    cf* A = tw + H;
+    cf* A = tw + H + a.plan.ntab;
     cf* B = A + (size_t)H * cols;
-    for (int i = threadIdx.x; i < H; i += blockDim.x) tw[i] = a.tw[i];
+    cf* X = B + (size_t)H * cols;
+    for (int i = threadIdx.x; i < H + a.plan.ntab; i += blockDim.x) tw[i] = a.tw[i];
     const long long p = blockIdx.x / a.colblocks;
     const int c0 = (int)(blockIdx.x % a.colblocks) * cols;
     const int nc = min(cols, Wh - c0);
@@ -318,7 +432,7 @@ __global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
         A[i * cols + c] = c < nc ? S[(size_t)i * Wh + c] : mkc(0.f, 0.f);
     }
     __syncthreads();
-    cf* res = gfft_lds<-1>(A, B, a.plan, cols, tw);
+    cf* res = gfft_lds<-1, BM>(A, B, a.plan, cols, tw, X);
     cf* other = (res == A) ? B : A;
     if (a.dump) {
         cf* D = a.dump + (size_t)p * H * Wh + c0;
@@ -339,7 +453,7 @@ __global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
         res[ky * cols + c] = v;
     }
     __syncthreads();
-    const cf* out = gfft_lds<+1>(res, other, a.plan, cols, tw);
+    const cf* out = gfft_lds<+1, BM>(res, other, a.plan, cols, tw, X);
     for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
         const int i = idx / cols, c = idx % cols;
         if (c < nc) S[(size_t)i * Wh + c] = out[i * cols + c];
