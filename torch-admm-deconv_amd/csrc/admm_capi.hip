@@ -483,6 +483,12 @@ GPlan make_plan_radices(int n);
 // larger primes keep the O(R)-per-output stage.  ADMM_BLUE_MIN <= 0 disables it (A/B).
 int blue_min() { return env_int("ADMM_BLUE_MIN", 41); }
 
+constexpr size_t kMaxLds = 160 * 1024;
+// LDS bytes of a generic transform kernel: twiddles + tables, two line buffers, Bluestein exchange
+size_t glds(int n, int lines, const GPlan& p) {
+    return sizeof(cf) * ((size_t)n * (1 + 2 * (size_t)lines) + p.ntab + p.xslots);
+}
+
 GPlan make_plan(int n) {
     GPlan p = make_plan_radices(n);
     const int bmin = blue_min();
@@ -505,6 +511,7 @@ GPlan make_plan(int n) {
     p.bm = M;
     p.ntab = off - n;
     p.xslots = M > 0 ? (256 / (M / blue_e(M))) * (M + M / 8) : 0;
+    if (M > 0 && glds(n, 1, p) > kMaxLds) return make_plan_radices(n);  // one line must fit the LDS
     return p;
 }
 
@@ -563,18 +570,33 @@ int pow2_floor(int v) { int p = 1; while (2 * p <= v) p *= 2; return p; }
 // LDS image <= ~32 KB (4+ resident blocks per CU: the prime-radix stages are latency-bound
 // chains and need the waves), except where one line alone is bigger
 // (A/B knobs ADMM_GROW_LINES / ADMM_GCOL_COLS: rounded down to a power of two in [1, 32])
-int grow_lines(int W) {
-    const int dflt = pow2_floor(std::max(1, std::min(32, (4096 / W - 1) / 2)));
-    return pow2_floor(std::max(1, std::min(32, env_int("ADMM_GROW_LINES", dflt))));
+// With Bluestein stages the column pass takes at least as many columns as make one item per
+// sub-group (16x3x509^2: 2 -> 4 columns, 1,125 -> 1,368 it/s; BSD keeps 4).  Either count is
+// halved until the block's LDS fits.
+int fit_lines(int n, int lines, const GPlan& p) {
+    while (lines > 1 && glds(n, lines, p) > kMaxLds) lines /= 2;
+    return lines;
 }
-int gcol_cols(int H) {
-    const int dflt = pow2_floor(std::max(1, std::min(16, (4096 / H - 1) / 2)));
-    return pow2_floor(std::max(1, std::min(32, env_int("ADMM_GCOL_COLS", dflt))));
+int grow_lines(int W, const GPlan& p) {
+    const int dflt = pow2_floor(std::max(1, std::min(32, (4096 / W - 1) / 2)));
+    return fit_lines(W, pow2_floor(std::max(1, std::min(32, env_int("ADMM_GROW_LINES", dflt)))), p);
+}
+int gcol_cols(int H, const GPlan& p) {
+    int dflt = pow2_floor(std::max(1, std::min(16, (4096 / H - 1) / 2)));
+    if (p.bm > 0) {
+        int nb = H;  // butterflies per line of the Bluestein stages (fewest)
+        for (int s = 0; s < p.nst; ++s)
+            if (p.bst[s] > 0) nb = std::min(nb, H / p.rad[s]);
+        const int nsg = 256 / (p.bm / blue_e(p.bm));
+        while (dflt * nb < nsg && dflt < 16) dflt *= 2;
+    }
+    return fit_lines(H, pow2_floor(std::max(1, std::min(32, env_int("ADMM_GCOL_COLS", dflt)))), p);
 }
 
 int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hipStream_t s) {
-    GRowArgs a{img, spec, nullptr, tw, make_plan(W), rows, grow_lines(W)};
-    const size_t lds = sizeof(cf) * ((size_t)W * (1 + 2 * a.lines) + a.plan.ntab + a.plan.xslots);
+    const GPlan pl = make_plan(W);
+    GRowArgs a{img, spec, nullptr, tw, pl, rows, grow_lines(W, pl)};
+    const size_t lds = glds(W, a.lines, a.plan);
     return with_bm(a.plan.bm, [&](auto bm) {
         constexpr int BM = decltype(bm)::value;
         if (int e = set_lds(k_grow_fwd<BM>, lds)) return e;
@@ -583,8 +605,9 @@ int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hi
     });
 }
 int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hipStream_t s) {
-    GRowArgs a{nullptr, const_cast<cf*>(spec), img, tw, make_plan(W), rows, grow_lines(W)};
-    const size_t lds = sizeof(cf) * ((size_t)W * (1 + 2 * a.lines) + a.plan.ntab + a.plan.xslots);
+    const GPlan pl = make_plan(W);
+    GRowArgs a{nullptr, const_cast<cf*>(spec), img, tw, pl, rows, grow_lines(W, pl)};
+    const size_t lds = glds(W, a.lines, a.plan);
     return with_bm(a.plan.bm, [&](auto bm) {
         constexpr int BM = decltype(bm)::value;
         if (int e = set_lds(k_grow_inv<BM>, lds)) return e;
@@ -599,10 +622,11 @@ template <int MODE, int BM> int gcol_launch(const GColArgs& a, size_t lds, dim3 
 }
 int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H, int W, long long P, int mode,
          hipStream_t s) {
-    const int Wh = W / 2 + 1, cols = gcol_cols(H);
+    const GPlan pl = make_plan(H);
+    const int Wh = W / 2 + 1, cols = gcol_cols(H, pl);
     const int colblocks = (Wh + cols - 1) / cols;
-    GColArgs a{spec, dump, fcT, mT, tw, make_plan(H), Wh, cols, colblocks, P};
-    const size_t lds = sizeof(cf) * ((size_t)H * (1 + 2 * cols) + a.plan.ntab + a.plan.xslots);
+    GColArgs a{spec, dump, fcT, mT, tw, pl, Wh, cols, colblocks, P};
+    const size_t lds = glds(H, cols, a.plan);
     const dim3 grid((unsigned)(P * colblocks));
     return with_bm(a.plan.bm, [&](auto bm) {
         constexpr int BM = decltype(bm)::value;
