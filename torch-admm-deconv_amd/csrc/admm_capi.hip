@@ -547,6 +547,12 @@ GPlan make_plan_radices(int n) {
             for (int q = 3; q * q <= f; q += 2) prime = prime && (f % q) != 0;
             if (prime) take_all(f);
         }
+        // powers of two as radix-16 / 8 stages (one LDS round trip per 16 / 8 instead of two /
+        // three radix-4 / 2 ones); ADMM_GPLAN_R16=0 for the radix-4/2 plan (A/B)
+        if (env_int("ADMM_GPLAN_R16", 1)) {
+            take_all(16);
+            take_all(8);
+        }
         take_all(4);
         take_all(2);
         take_all(3);

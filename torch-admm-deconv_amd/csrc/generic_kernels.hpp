@@ -65,6 +65,8 @@ __device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw,
         v[2] = csub(t0, t2);
         v[1] = cadd(t1, t3);
         v[3] = csub(t1, t3);
+    } else if constexpr (R == 8 || R == 16) {
+        DFT<R, DIR>::template run<1, 0>(v);  // register DFT with exact constant twiddles (fft_core.hpp)
     } else {
         // y_k = sum_q v_q W_R^{qk}, W_R^j = tw[j n / R]
         cf y[R];
@@ -261,6 +263,8 @@ __device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf
                 case 2: gstage_r<DIR, 2>(src, dst, pl.n, NS, lines, tw); break;
                 case 3: gstage_r<DIR, 3>(src, dst, pl.n, NS, lines, tw); break;
                 case 4: gstage_r<DIR, 4>(src, dst, pl.n, NS, lines, tw); break;
+                case 8: gstage_r<DIR, 8>(src, dst, pl.n, NS, lines, tw); break;
+                case 16: gstage_r<DIR, 16>(src, dst, pl.n, NS, lines, tw); break;
                 case 5: gstage_r<DIR, 5>(src, dst, pl.n, NS, lines, tw); break;
                 case 7: gstage_r<DIR, 7>(src, dst, pl.n, NS, lines, tw); break;
                 default: gstage_any<DIR>(src, dst, pl.n, NS, R, lines, tw); break;
