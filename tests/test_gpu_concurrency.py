@@ -90,15 +90,17 @@ def test_profiler_totals_under_threads(cuda_dev):
 
 
 def test_double_backward_is_not_supported(cuda_dev):
+    """Differentiating the gradient again raises (the backward op has no autograd formula); a second
+    backward with retain_graph=True reuses the kept history and gives the same gradient."""
     from admmtor.eops.deconv import fft_admm_tv
     x, k, _ = _case(cuda_dev, True, 6)
     xg = x.clone().requires_grad_(True)
     out = fft_admm_tv(xg, 0.01, 0.02, k, True, 10)
     (g,) = torch.autograd.grad(out.square().sum(), xg, create_graph=True)
-    with pytest.raises(RuntimeError, match="once_differentiable|differentiate"):
+    with pytest.raises(RuntimeError, match="no autograd formula|once_differentiable|differentiate"):
         g.sum().backward()
     out = fft_admm_tv(xg, 0.01, 0.02, k, True, 10)
     loss = out.square().sum()
-    loss.backward(retain_graph=True)
-    with pytest.raises(RuntimeError, match="backward through it twice"):
-        loss.backward()
+    (g1,) = torch.autograd.grad(loss, xg, retain_graph=True)
+    (g2,) = torch.autograd.grad(loss, xg)
+    assert torch.equal(g1, g2)

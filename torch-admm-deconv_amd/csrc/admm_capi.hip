@@ -588,7 +588,9 @@ int grow_lines(int W, const GPlan& p) {
     return fit_lines(W, pow2_floor(std::max(1, std::min(32, env_int("ADMM_GROW_LINES", dflt)))), p);
 }
 int gcol_cols(int H, const GPlan& p) {
-    int dflt = pow2_floor(std::max(1, std::min(16, (4096 / H - 1) / 2)));
+    // column blocks: ~48 KB LDS images without Bluestein stages (VGA 480: 2 -> 4 columns +7 %,
+    // 500: +4 %, HD 1080: 1 -> 2 columns +6 %; tools/bench_generic_sizes.py), ~32 KB with them
+    int dflt = pow2_floor(std::max(1, std::min(16, ((p.bm > 0 ? 4096 : 6144) / H - 1) / 2)));
     if (p.bm > 0) {
         int nb = H;  // butterflies per line of the Bluestein stages (fewest)
         for (int s = 0; s < p.nst; ++s)
