@@ -131,6 +131,51 @@ def cpu_baseline(cfg, planes, iters):
                       f"value scaled by planes {nb * C}/{B * C}; CPU: {cpu}"}
 
 
+def cpu_baseline_c5(H=128, B=1, steps=2):
+    """C5 on the host cores: the same training step (DivergentRestorer, two learnable iso ADMM
+    modules of 100 iterations, L1 loss, AdamW) in fp32 on a bounded sample, with the solver
+    routed to the oracle's restatement of the reference op sequence (solve_spatial, autograd
+    through it, as the reference trains) -- the reference's CPU path.  Scaled by pixels to the
+    C5 batch (16 x 3 x 512^2)."""
+    import admmtor.elayers.admmdeconv as admmdeconv
+    from admmtor.modelbuild.denoiser import DivergentRestorer
+    from admmtor.synth import CONFIG_SEED, clean_images
+    from oracle.admm_oracle import solve_spatial
+    ncores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores))))
+    Bc, C, Hc, Wc, _, _, maxit, _, _ = CONFIGS["c5"]
+    solver = admmdeconv.fft_admm_tv
+    admmdeconv.fft_admm_tv = lambda x, l, r, k, iso, it: solve_spatial(x, l, r, k, iso, it)
+    try:
+        deconv = {"kern_size": (), "max_iters": maxit, "iso": True}
+        torch.manual_seed(CONFIG_SEED + 5)
+        model = DivergentRestorer([2, 8, 32], 3, 3, 86, 86, 8, output_activation=torch.nn.Sigmoid(),
+                                  admms=[dict(deconv), dict(deconv)])
+        opt = torch.optim.AdamW(model.parameters(), 8.8e-4, betas=(0.9, 0.9))
+        y = clean_images(B, C, H, H, seed=CONFIG_SEED + 5)
+        x = (y + 0.06 * torch.randn(y.shape, generator=torch.Generator().manual_seed(5))).clamp_(0, 1)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss = (model(x) - y).abs().mean()
+            loss.backward()
+            opt.step()
+        step()  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        admmdeconv.fft_admm_tv = solver
+    scale = (B * H * H) / (Bc * Hc * Wc)
+    return {"value": scale / dt, "unit": "C5-equivalent training steps/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{B}x{C}x{H}x{H} fp32, {steps} steps after 1 warm-up, {dt:.2f} s/step; solver = "
+                      f"oracle/admm_oracle.py solve_spatial (reference op sequence, autograd), CNN = this "
+                      f"build's state-dict-compatible modules on the CPU; value scaled by pixels "
+                      f"{B * H * H}/{Bc * Hc * Wc}"}
+
+
 def run_c5(args, world, rank, dev):
     """Config 5: one training step of the reference's training model
     (scripts/train.py:70-73: two learnable iso ADMM-TV modules, 100 iterations each, then the
@@ -225,7 +270,9 @@ def run_c5(args, world, rank, dev):
             "admm_share": {"ms_per_step_in_admm_kernels": admm_ms / K, "fraction": admm_ms / 1e3 / T,
                            "launches_per_step": sum(cnt) / K},
             "peak_mem_GiB": torch.cuda.max_memory_allocated(dev) / 2**30,
-            "loss": float(loss.detach()), "cpu_baseline": None}), flush=True)
+            "loss": float(loss.detach()),
+            "cpu_baseline": cpu_baseline_c5() if (world == 1 and not args.no_cpu_baseline) else None}),
+              flush=True)
 
 
 def main():

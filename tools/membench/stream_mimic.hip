@@ -418,6 +418,28 @@ int main() {
         printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
     const double arr = (double)n * sizeof(cf);
+    if (getenv("STAGGER_SWEEP")) {
+        // pass A's 7 streams carved from one allocation with a stagger between arrays: do the
+        // same (plane, row) offsets of different arrays collide in HBM channels when the arrays
+        // start at multiples of 768 MiB?
+        const long long ns = (long long)P * H / 8;
+        const size_t stg_max = 1 << 20;
+        char* big;
+        CK(hipMalloc(&big, 7 * ((size_t)arr + stg_max) + 4096));
+        CK(hipMemset(big, 0, 7 * ((size_t)arr + stg_max) + 4096));
+        const size_t strides[] = {0, 256, 2048, 4096 + 256, 16384 + 512, 65536 + 4096, 262144 + 8192, 1048576};
+        for (int rep = 0; rep < 2; ++rep)
+            for (size_t sg : strides) {
+                cf* a[7];
+                for (int i = 0; i < 7; ++i) a[i] = reinterpret_cast<cf*>(big + (size_t)i * ((size_t)arr + sg));
+                char name[64];
+                snprintf(name, sizeof name, "A nt stagger %zu B", sg);
+                timeit(name, 7 * arr, [&] { k_mimic<8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(a[0], a[1], a[2], a[3], a[4], a[5], a[6], H, ns); });
+                snprintf(name, sizeof name, "B remap in place stagger %zu B", sg);
+                timeit(name, 2 * arr, [&] { k_colmimic_mix<512, 8, false, false, true><<<(unsigned)(P * (N / 8)), 512>>>(a[6], a[6], H, N / 8); });
+            }
+        return 0;
+    }
     if (getenv("MIXED_SWEEP2")) {
         const long long ns = (long long)P * H / 8;
         const int colblocks = N / 8;
