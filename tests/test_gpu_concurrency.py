@@ -104,3 +104,29 @@ def test_double_backward_is_not_supported(cuda_dev):
     (g1,) = torch.autograd.grad(loss, xg, retain_graph=True)
     (g2,) = torch.autograd.grad(loss, xg)
     assert torch.equal(g1, g2)
+
+
+@pytest.mark.parametrize("iso", [False, True])
+def test_solver_is_graph_capturable(cuda_dev, iso):
+    """The solve enqueues only asynchronous work on the current stream (no host synchronisation,
+    workspace from the caching allocator): it can be captured in a HIP graph (torch.cuda.CUDAGraph)
+    and replayed, giving the eager result bit for bit (include/admm_tv.h: graph-capturable)."""
+    from admmtor.eops.deconv import fft_admm_tv
+    x, k, _ = _case(cuda_dev, iso, 6)
+    static_x = x.clone()
+    eager = fft_admm_tv(static_x, 0.01, 0.02, k, iso, 12)
+    s = torch.cuda.Stream(cuda_dev)
+    s.wait_stream(torch.cuda.current_stream(cuda_dev))
+    with torch.cuda.stream(s):  # warm-up on the side stream, as torch.cuda.graphs recommends
+        fft_admm_tv(static_x, 0.01, 0.02, k, iso, 12)
+    torch.cuda.current_stream(cuda_dev).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        static_out = fft_admm_tv(static_x, 0.01, 0.02, k, iso, 12)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(static_out, eager)
+    static_x.copy_(x.flip(-1))  # new input, same buffers
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(static_out, fft_admm_tv(x.flip(-1), 0.01, 0.02, k, iso, 12))
