@@ -36,7 +36,7 @@ extern "C" {
 enum {
     ADMM_TV_OK = 0,
     ADMM_TV_EINVAL = -1,        /* null pointer / negative sizes / maxit < 0       */
-    ADMM_TV_EUNSUPPORTED = -2,  /* H, W outside [1, 4096]; PSF gradient at a generic size */
+    ADMM_TV_EUNSUPPORTED = -2,  /* H, W not supported (admm_tv_supported == 0)               */
     ADMM_TV_ENONSQUARE = -3,    /* kh != kw  (reference: RuntimeError, deconv.py:90-96) */
     ADMM_TV_EWORKSPACE = -4,    /* workspace too small / misaligned                 */
     ADMM_TV_EHIP = -5,          /* a HIP runtime call or kernel launch failed       */
@@ -93,7 +93,8 @@ int admm_tv_abi_version(void);
 const char* admm_tv_build_hash(void);
 
 /* 1: (H, W) runs on the fused power-of-two kernels (H in [16,4096], W in [16,2048]);
- * 2: any other size in [1,4096] x [1,4096], run on the generic kernels (mixed-radix
+ * 2: any other size whose lines fit the generic kernels' LDS image (a line of n complex
+ *    values, its twiddles and Bluestein tables: n up to ~6,800), run on the generic kernels (mixed-radix
  *    transforms, per-pixel step; the reference accepts any size, deconv.py:103-106);
  * 0: unsupported. */
 int admm_tv_supported(int64_t H, int64_t W);

@@ -65,6 +65,8 @@ def test_g7_odd_size_vs_reference(cuda_dev):
     ((1, 1, 509, 37), ("motion", 9), False, 10),           # prime 509: Bluestein at M = 1024
     ((1, 2, 26, 1021), None, False, 8),                    # prime 1021 > 512: the direct prime stage
     ((1, 1, 214, 321), ("gauss:2", 7), True, 12),          # 2*107 x 3*107
+    ((1, 1, 12, 6000), ("gauss:1.5", 9), False, 6),        # lines beyond 4096 (one line per block)
+    ((1, 1, 5120, 9), ("motion", 5), True, 5),             # a 5120-point column pass
 ])
 def test_generic_shapes_vs_oracle(cuda_dev, shape, psf, iso, it):
     from admmtor.synth import blurred_batch, make_psf

@@ -64,7 +64,8 @@ def fft_admm_tv_fwd(x: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso: bool
     lib = _native.load()
     B, C, H, W = x.shape
     if not _native.supported(H, W):
-        raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} outside [1, 4096]")
+        raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
+                                  "size whose lines fit the generic kernels' LDS, up to ~6,800)")
     d = _desc(x, lam, kern, iso, maxit)
     x, lam, rho, kern = x.contiguous(), lam.contiguous(), rho.contiguous(), kern.contiguous()
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x.device)
@@ -95,7 +96,8 @@ def fft_admm_tv_fwd_train(x: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso
     lib = _native.load()
     B, C, H, W = x.shape
     if not _native.supported(H, W):
-        raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} outside [1, 4096]")
+        raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
+                                  "size whose lines fit the generic kernels' LDS, up to ~6,800)")
     d = _desc(x, lam, kern, iso, maxit, _flags(kern, psf_grad))
     x, lam, rho, kern = x.contiguous(), lam.contiguous(), rho.contiguous(), kern.contiguous()
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x.device)

@@ -90,10 +90,13 @@ bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 bool supported_hw(int64_t H, int64_t W) {
     return pow2(H) && pow2(W) && H >= 16 && H <= 4096 && W >= 16 && W <= 2048;
 }
-// any other size up to 4096 x 4096 runs on the generic kernels (generic_kernels.hpp)
-constexpr int64_t kGenericMax = 4096;
+// any other size runs on the generic kernels (generic_kernels.hpp), as long as one line of each
+// dimension fits their LDS image (twiddles + two line buffers + Bluestein tables): up to ~6,800
+constexpr int64_t kGenericMax = 8192;
+bool gen_fits(int n);  // below, with the plans
 bool generic_hw(int64_t H, int64_t W) {
-    return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax;
+    return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax && gen_fits((int)H) &&
+           gen_fits((int)W);
 }
 
 int env_int(const char* name, int dflt) {
@@ -388,7 +391,7 @@ int validate(const admm_tv_desc* d) {
         return fail(ADMM_TV_EINVAL, "invalid sizes or maxit");
     if (d->kh != d->kw) return fail(ADMM_TV_ENONSQUARE, "non-square PSF (the reference's H_t swaps H/W pads)");
     if (!supported_hw(d->H, d->W) && !generic_hw(d->H, d->W))
-        return fail(ADMM_TV_EUNSUPPORTED, "H and W must be in [1, 4096]");
+        return fail(ADMM_TV_EUNSUPPORTED, "unsupported H, W (admm_tv_supported: generic sizes up to ~6,800)");
     if (d->kh > d->H || d->kw > d->W) return fail(ADMM_TV_EKERNEL, "PSF larger than the image");
     if (d->groups > 1 && (!supported_hw(d->H, d->W) || (d->flags & ADMM_TV_FLAG_PSF_GRAD)))
         return fail(ADMM_TV_EUNSUPPORTED, "groups > 1 needs power-of-two H, W and no PSF gradient");
@@ -515,6 +518,8 @@ GPlan make_plan(int n) {
     return p;
 }
 
+bool gen_fits(int n) { return glds(n, 1, make_plan(n)) <= kMaxLds; }
+
 // the kernel instantiation for a plan's Bluestein size
 template <class F> int with_bm(int bm, F&& f) {
     switch (bm) {
@@ -542,11 +547,16 @@ GPlan make_plan_radices(int n) {
     if (env_int("ADMM_GPLAN_PRIME_FIRST", 1)) {
         // any other prime first: at NS = 1 its stage needs no twiddle pass (BSD size: column pass
         // 122 -> 112 ms per 250 launches, 1,410 -> 1,491 it/s)
-        for (int f = 11; f <= n; f += 2) {
-            bool prime = true;
-            for (int q = 3; q * q <= f; q += 2) prime = prime && (f % q) != 0;
-            if (prime) take_all(f);
-        }
+        // (the primes >= 11 of n by trial division of n stripped of 2, 3, 5, 7: O(sqrt n))
+        int r = n;
+        for (int q : {2, 3, 5, 7})
+            while (r % q == 0) r /= q;
+        for (int f = 11; f * f <= r; f += 2)
+            if (r % f == 0) {
+                take_all(f);
+                while (r % f == 0) r /= f;
+            }
+        if (r > 1) take_all(r);
         // powers of two as radix-16 / 8 stages (one LDS round trip per 16 / 8 instead of two /
         // three radix-4 / 2 ones); ADMM_GPLAN_R16=0 for the radix-4/2 plan (A/B)
         if (env_int("ADMM_GPLAN_R16", 1)) {
@@ -565,7 +575,8 @@ GPlan make_plan_radices(int n) {
     take_all(3);
     take_all(5);
     take_all(7);
-    for (int f = 11; f <= n && m > 1; f += 2) take_all(f);  // any other prime: O(R) per output
+    for (int f = 11; f * f <= m; f += 2) take_all(f);  // any other prime: O(R) per output
+    if (m > 1) take_all(m);
     return p;
 }
 
