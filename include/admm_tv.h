@@ -93,8 +93,8 @@ int admm_tv_abi_version(void);
 const char* admm_tv_build_hash(void);
 
 /* 1: (H, W) runs on the fused power-of-two kernels (H in [16,4096], W in [16,2048]);
- * 2: any other size whose lines fit the generic kernels' LDS image (a line of n complex
- *    values, its twiddles and Bluestein tables: n up to ~6,800), run on the generic kernels (mixed-radix
+ * 2: any other size whose lines fit the generic kernels' LDS image (two buffers of a line of
+ *    n complex values: n up to 10,240), run on the generic kernels (mixed-radix
  *    transforms, per-pixel step; the reference accepts any size, deconv.py:103-106);
  * 0: unsupported. */
 int admm_tv_supported(int64_t H, int64_t W);

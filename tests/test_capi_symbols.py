@@ -54,7 +54,7 @@ def test_host_entry_points():
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
     assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 4096), (8, 64), (1, 1), (481, 321))] == [generic] * 5
     assert [lib.admm_tv_supported(*hw) for hw in ((4097, 16), (5000, 33))] == [generic] * 2  # beyond 4096
-    assert [lib.admm_tv_supported(*hw) for hw in ((7000, 16), (16, 8192), (0, 16))] == [0] * 3
+    assert [lib.admm_tv_supported(*hw) for hw in ((10241, 16), (16, 12288), (0, 16))] == [0] * 3
     d = _native.desc(64, 3, 1024, 1024, 21, False, 50)
     ws = _native.workspace_size(d)
     img = 64 * 3 * 1024 * 1024 * 4
@@ -65,7 +65,7 @@ def test_host_entry_points():
 
 @pytest.mark.parametrize("field,value,code", [
     ("kw", 5, -3),      # non-square PSF -> ADMM_TV_ENONSQUARE
-    ("H", 7000, -2),    # unsupported size (a 7000-point line exceeds the generic kernels' LDS)
+    ("H", 10241, -2),   # unsupported size (a line longer than the generic kernels' LDS image)
     ("maxit", -1, -1),  # invalid
     ("kh", 99, -3),
 ])
@@ -125,11 +125,13 @@ def test_library_built_from_this_tree():
 
 def test_supported_sizes():
     """admm_tv_supported (host-only): power-of-two sizes on the fused kernels (1), any other size
-    whose lines fit the generic kernels' LDS image (2; up to ~6,800 per side), else 0."""
+    whose lines fit the generic kernels' LDS image (2; twiddles move to global memory beyond ~6,800
+    points; up to 10,240 per side), else 0."""
     from admmtor import _native
     L = _native.load()
     assert L.admm_tv_supported(1024, 1024) == 1 and L.admm_tv_supported(4096, 2048) == 1
     assert L.admm_tv_supported(15, 17) == 2 and L.admm_tv_supported(4096, 4096) == 2
     assert L.admm_tv_supported(6000, 4000) == 2 and L.admm_tv_supported(6800, 16) == 2
-    assert L.admm_tv_supported(7000, 16) == 0 and L.admm_tv_supported(8192, 8192) == 0
+    assert L.admm_tv_supported(7680, 4320) == 2 and L.admm_tv_supported(8192, 8192) == 2  # global twiddles
+    assert L.admm_tv_supported(10240, 16) == 2 and L.admm_tv_supported(10241, 16) == 0
     assert L.admm_tv_supported(0, 16) == 0

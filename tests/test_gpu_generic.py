@@ -67,6 +67,8 @@ def test_g7_odd_size_vs_reference(cuda_dev):
     ((1, 1, 214, 321), ("gauss:2", 7), True, 12),          # 2*107 x 3*107
     ((1, 1, 12, 6000), ("gauss:1.5", 9), False, 6),        # lines beyond 4096 (one line per block)
     ((1, 1, 5120, 9), ("motion", 5), True, 5),             # a 5120-point column pass
+    ((1, 1, 10, 8192), ("gauss:1.5", 9), False, 4),        # 8192-point rows: twiddles from global memory
+    ((1, 1, 7680, 6), None, True, 4),                      # 7680-point columns (an 8K frame width)
 ])
 def test_generic_shapes_vs_oracle(cuda_dev, shape, psf, iso, it):
     from admmtor.synth import blurred_batch, make_psf

@@ -65,7 +65,7 @@ def fft_admm_tv_fwd(x: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso: bool
     B, C, H, W = x.shape
     if not _native.supported(H, W):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
-                                  "size whose lines fit the generic kernels' LDS, up to ~6,800)")
+                                  "size whose lines fit the generic kernels' LDS, up to 10,240)")
     d = _desc(x, lam, kern, iso, maxit)
     x, lam, rho, kern = x.contiguous(), lam.contiguous(), rho.contiguous(), kern.contiguous()
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x.device)
@@ -97,7 +97,7 @@ def fft_admm_tv_fwd_train(x: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso
     B, C, H, W = x.shape
     if not _native.supported(H, W):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
-                                  "size whose lines fit the generic kernels' LDS, up to ~6,800)")
+                                  "size whose lines fit the generic kernels' LDS, up to 10,240)")
     d = _desc(x, lam, kern, iso, maxit, _flags(kern, psf_grad))
     x, lam, rho, kern = x.contiguous(), lam.contiguous(), rho.contiguous(), kern.contiguous()
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x.device)

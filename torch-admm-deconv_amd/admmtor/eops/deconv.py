@@ -148,7 +148,7 @@ def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.T
     d = _native.desc(B, C, H, W, k, iso, maxit, 0, G, bound)
     if not _native.supported(H, W):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
-                                  "size whose lines fit the generic kernels' LDS, up to ~6,800)")
+                                  "size whose lines fit the generic kernels' LDS, up to 10,240)")
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
     bound.add(ws)
     out = torch.empty((G * B, C, H, W), dtype=torch.float32, device=x32.device)

@@ -91,8 +91,9 @@ bool supported_hw(int64_t H, int64_t W) {
     return pow2(H) && pow2(W) && H >= 16 && H <= 4096 && W >= 16 && W <= 2048;
 }
 // any other size runs on the generic kernels (generic_kernels.hpp), as long as one line of each
-// dimension fits their LDS image (twiddles + two line buffers + Bluestein tables): up to ~6,800
-constexpr int64_t kGenericMax = 8192;
+// dimension fits their LDS image (two line buffers + twiddles and Bluestein tables, the latter read
+// from global memory for lines beyond ~6,800 points): up to 10,240
+constexpr int64_t kGenericMax = 10240;
 bool gen_fits(int n);  // below, with the plans
 bool generic_hw(int64_t H, int64_t W) {
     return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax && gen_fits((int)H) &&
@@ -489,7 +490,7 @@ int blue_min() { return env_int("ADMM_BLUE_MIN", 41); }
 constexpr size_t kMaxLds = 160 * 1024;
 // LDS bytes of a generic transform kernel: twiddles + tables, two line buffers, Bluestein exchange
 size_t glds(int n, int lines, const GPlan& p) {
-    return sizeof(cf) * ((size_t)n * (1 + 2 * (size_t)lines) + p.ntab + p.xslots);
+    return sizeof(cf) * ((p.twg ? 0 : (size_t)n + p.ntab) + 2 * (size_t)n * lines + p.xslots);
 }
 
 GPlan make_plan(int n) {
@@ -514,14 +515,23 @@ GPlan make_plan(int n) {
     p.bm = M;
     p.ntab = off - n;
     p.xslots = M > 0 ? (256 / (M / blue_e(M))) * (M + M / 8) : 0;
-    if (M > 0 && glds(n, 1, p) > kMaxLds) return make_plan_radices(n);  // one line must fit the LDS
-    return p;
+    // one line must fit the LDS: else no Bluestein, else twiddles from global memory
+    if (glds(n, 1, p) <= kMaxLds) return p;
+    GPlan q = make_plan_radices(n);
+    q.twg = glds(n, 1, q) > kMaxLds ? 1 : 0;
+    return q;
 }
 
 bool gen_fits(int n) { return glds(n, 1, make_plan(n)) <= kMaxLds; }
 
+template <class F> int with_plan(const GPlan& p, F&& f) {
+    if (p.twg) return f(std::integral_constant<int, 0>{}, std::true_type{});
+    return with_bm(p.bm, [&](auto bm) { return f(bm, std::false_type{}); });
+}
+
 // the kernel instantiation for a plan's Bluestein size
 template <class F> int with_bm(int bm, F&& f) {
+    // f(integral_constant BM, bool_constant TWG): global-memory twiddles only on plans without Bluestein
     switch (bm) {
         case 0: return f(std::integral_constant<int, 0>{});
         case 32: return f(std::integral_constant<int, 32>{});
@@ -616,10 +626,11 @@ int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hi
     const GPlan pl = make_plan(W);
     GRowArgs a{img, spec, nullptr, tw, pl, rows, grow_lines(W, pl)};
     const size_t lds = glds(W, a.lines, a.plan);
-    return with_bm(a.plan.bm, [&](auto bm) {
+    return with_plan(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
-        if (int e = set_lds(k_grow_fwd<BM>, lds)) return e;
-        hipLaunchKernelGGL(k_grow_fwd<BM>, dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
+        constexpr bool TWG = decltype(twg)::value;
+        if (int e = set_lds(k_grow_fwd<BM, TWG>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_fwd<BM, TWG>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
         return launch_check("k_grow_fwd");
     });
 }
@@ -627,16 +638,17 @@ int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hi
     const GPlan pl = make_plan(W);
     GRowArgs a{nullptr, const_cast<cf*>(spec), img, tw, pl, rows, grow_lines(W, pl)};
     const size_t lds = glds(W, a.lines, a.plan);
-    return with_bm(a.plan.bm, [&](auto bm) {
+    return with_plan(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
-        if (int e = set_lds(k_grow_inv<BM>, lds)) return e;
-        hipLaunchKernelGGL(k_grow_inv<BM>, dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
+        constexpr bool TWG = decltype(twg)::value;
+        if (int e = set_lds(k_grow_inv<BM, TWG>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_inv<BM, TWG>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
         return launch_check("k_grow_inv");
     });
 }
-template <int MODE, int BM> int gcol_launch(const GColArgs& a, size_t lds, dim3 grid, hipStream_t s) {
-    if (int e = set_lds(k_gcol<MODE, BM>, lds)) return e;
-    hipLaunchKernelGGL((k_gcol<MODE, BM>), grid, dim3(256), lds, s, a);
+template <int MODE, int BM, bool TWG> int gcol_launch(const GColArgs& a, size_t lds, dim3 grid, hipStream_t s) {
+    if (int e = set_lds(k_gcol<MODE, BM, TWG>, lds)) return e;
+    hipLaunchKernelGGL((k_gcol<MODE, BM, TWG>), grid, dim3(256), lds, s, a);
     return launch_check("k_gcol");
 }
 int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H, int W, long long P, int mode,
@@ -647,13 +659,14 @@ int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H
     GColArgs a{spec, dump, fcT, mT, tw, pl, Wh, cols, colblocks, P};
     const size_t lds = glds(H, cols, a.plan);
     const dim3 grid((unsigned)(P * colblocks));
-    return with_bm(a.plan.bm, [&](auto bm) {
+    return with_plan(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
+        constexpr bool TWG = decltype(twg)::value;
         switch (mode) {
-            case 0: return gcol_launch<0, BM>(a, lds, grid, s);
-            case 1: return gcol_launch<1, BM>(a, lds, grid, s);
-            case 2: return gcol_launch<2, BM>(a, lds, grid, s);
-            default: return gcol_launch<3, BM>(a, lds, grid, s);
+            case 0: return gcol_launch<0, BM, TWG>(a, lds, grid, s);
+            case 1: return gcol_launch<1, BM, TWG>(a, lds, grid, s);
+            case 2: return gcol_launch<2, BM, TWG>(a, lds, grid, s);
+            default: return gcol_launch<3, BM, TWG>(a, lds, grid, s);
         }
     });
 }

@@ -37,6 +37,8 @@ struct GPlan {
     int ntab;          // table entries after the n twiddles
     int xslots;        // exchange slots (complex values) the Bluestein stages need
     int bm;            // the plan's Bluestein size M (all its Bluestein stages), 0: none
+    int twg;           // 1: twiddles and tables are read from global memory (L1/L2), not LDS --
+                       // long lines (> ~6,800 points) whose LDS image would not fit otherwise
 };
 
 // values per lane of the power-of-two transform of length M (fft_core.hpp RowCfg)
@@ -331,15 +333,19 @@ struct GRowArgs {
 // Real rows are transformed two at a time: rows a, b as one complex row z = a + i b, whose
 // spectrum Z gives A[k] = (Z[k] + conj Z[-k]) / 2 and B[k] = (Z[k] - conj Z[-k]) / 2i.  A block
 // holds `lines` complex rows = 2 * lines real rows.
-template <int BM>
+// TWG: twiddles / tables read from global memory (GPlan::twg; a template parameter, so the LDS
+// variant keeps its LDS reads)
+template <int BM, bool TWG>
 __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
-    cf* tw = reinterpret_cast<cf*>(smem);
-    cf* A = tw + W + a.plan.ntab;
+    cf* twl = reinterpret_cast<cf*>(smem);
+    cf* A = twl + (TWG ? 0 : W + a.plan.ntab);
     cf* B = A + (size_t)W * lines;
     cf* X = B + (size_t)W * lines;  // Bluestein exchange slots
-    for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) tw[i] = a.tw[i];
+    if constexpr (!TWG)
+        for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
+    const cf* tw = TWG ? a.tw : twl;
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);  // real rows in this block
     for (int idx = threadIdx.x; idx < W * 2 * lines; idx += blockDim.x) {
@@ -360,15 +366,17 @@ __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
     }
 }
 
-template <int BM>
+template <int BM, bool TWG>
 __global__ void __launch_bounds__(256) k_grow_inv(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
-    cf* tw = reinterpret_cast<cf*>(smem);
-    cf* A = tw + W + a.plan.ntab;
+    cf* twl = reinterpret_cast<cf*>(smem);
+    cf* A = twl + (TWG ? 0 : W + a.plan.ntab);
     cf* B = A + (size_t)W * lines;
     cf* X = B + (size_t)W * lines;
-    for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) tw[i] = a.tw[i];
+    if constexpr (!TWG)
+        for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
+    const cf* tw = TWG ? a.tw : twl;
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);
     // Hermitian completion of a half spectrum: X[k] = conj X[W - k] for k >= Wh; the imaginary
@@ -418,15 +426,17 @@ struct GColArgs {
     long long P;
 };
 
-template <int MODE, int BM>
+template <int MODE, int BM, bool TWG>
 __global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
-    cf* tw = reinterpret_cast<cf*>(smem);
-    cf* A = tw + H + a.plan.ntab;
+    cf* twl = reinterpret_cast<cf*>(smem);
+    cf* A = twl + (TWG ? 0 : H + a.plan.ntab);
     cf* B = A + (size_t)H * cols;
     cf* X = B + (size_t)H * cols;
-    for (int i = threadIdx.x; i < H + a.plan.ntab; i += blockDim.x) tw[i] = a.tw[i];
+    if constexpr (!TWG)
+        for (int i = threadIdx.x; i < H + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
+    const cf* tw = TWG ? a.tw : twl;
     const long long p = blockIdx.x / a.colblocks;
     const int c0 = (int)(blockIdx.x % a.colblocks) * cols;
     const int nc = min(cols, Wh - c0);
