@@ -418,6 +418,21 @@ int main() {
         printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
     const double arr = (double)n * sizeof(cf);
+    if (getenv("MIXED_SWEEP3")) {  // T = 2 row-pair tiles: pass B reads whole 128-B lines
+        const long long ns = (long long)P * H / 8;
+        const int colblocks = N / 8;
+        const int reps = getenv("ONCE") ? 1 : 3;
+        for (int rep = 0; rep < reps; ++rep) {
+            timeit("A row-major nt (prod) R=8", 7 * arr, [&] { k_mimic<8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A out-tiled T=2 nt st", 7 * arr, [&] { k_mimic_ot<8, 2, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A out-tiled T=2 plain st", 7 * arr, [&] { k_mimic_ot<8, 2, false><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("B row->row remap in place (prod)", 2 * arr, [&] { k_colmimic_mix<512, 8, false, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[6], H, colblocks); });
+            timeit("B tiled2->row remap oop", 2 * arr, [&] { k_colmimic_mix<512, 2, true, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+            timeit("B tiled2->tiled2 remap in place", 2 * arr, [&] { k_colmimic_mix<512, 2, true, true, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[6], H, colblocks); });
+            timeit("B row->row remap oop", 2 * arr, [&] { k_colmimic_mix<512, 8, false, false, true><<<(unsigned)(P * colblocks), 512>>>(buf[6], buf[0], H, colblocks); });
+        }
+        return 0;
+    }
     if (getenv("STAGGER_SWEEP")) {
         // pass A's 7 streams carved from one allocation with a stagger between arrays: do the
         // same (plane, row) offsets of different arrays collide in HBM channels when the arrays

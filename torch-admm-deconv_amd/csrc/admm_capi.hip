@@ -281,20 +281,29 @@ template <class F> int with_row(int N, F&& f) {
 }
 
 // ------------------------------------------------------------------ column-side ops (templated on H, C)
+// column-pass tile order (k_pass_b pb_tile): planes per group, 1 = plane-major.  Two planes at
+// H >= 1024 (C3 pass B 0.376 -> 0.362 ms, C3 iso 0.381 -> 0.369; 4 and 8 planes slower: DRAM
+// locality), plane-major below (C2: neutral).  A/B knob ADMM_PASSB_GROUP.
+int passb_order(int H) { return std::max(1, std::min(64, env_int("ADMM_PASSB_GROUP", H >= 1024 ? 2 : 1))); }
+
 template <int H, int C> int pass_b_hc(const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N,
                                       int P, int mode, int ppm, hipStream_t s) {
     using G = ColGeom<H, C>;
     const int colblocks = N / C;
     const dim3 grid((unsigned)((long long)P * colblocks));
+    const int order = passb_order(H);
     if (mode == 0) {
         if (int e = set_lds(k_pass_b<H, C, 0>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm);
+        hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
+                           order);
     } else if (mode == 1) {
         if (int e = set_lds(k_pass_b<H, C, 1>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm);
+        hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
+                           order);
     } else {
         if (int e = set_lds(k_pass_b<H, C, 2>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm);
+        hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
+                           order);
     }
     return launch_check("k_pass_b");
 }
@@ -310,7 +319,7 @@ template <int H> int pass_b_h(const cf* spec, cf* out, const float* fcT, const c
             const int colblocks = N / 16;
             if (int e = set_lds(k_pass_b2<H, 8>, G::lds_bytes())) return e;
             hipLaunchKernelGGL((k_pass_b2<H, 8>), dim3((unsigned)((long long)P * colblocks)), dim3(G::NT), G::lds_bytes(),
-                               s, spec, out, fcT, twH, N, colblocks, ppm);
+                               s, spec, out, fcT, twH, N, colblocks, ppm, passb_order(H));
             return launch_check("k_pass_b2");
         }
         int C = env_int("ADMM_PASSB_C", 8);
@@ -524,6 +533,12 @@ GPlan make_plan(int n) {
 
 bool gen_fits(int n) { return glds(n, 1, make_plan(n)) <= kMaxLds; }
 
+// threads per block of the generic transform kernels (A/B knob; 64, 128 or 256)
+int gen_threads(const char* knob) {
+    const int v = env_int(knob, 256);
+    return v <= 64 ? 64 : v <= 128 ? 128 : 256;
+}
+
 template <class F> int with_plan(const GPlan& p, F&& f) {
     if (p.twg) return f(std::integral_constant<int, 0>{}, std::true_type{});
     return with_bm(p.bm, [&](auto bm) { return f(bm, std::false_type{}); });
@@ -630,7 +645,8 @@ int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hi
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
         if (int e = set_lds(k_grow_fwd<BM, TWG>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_fwd<BM, TWG>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_grow_fwd<BM, TWG>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))),
+                           dim3(gen_threads("ADMM_GROW_NT")), lds, s, a);
         return launch_check("k_grow_fwd");
     });
 }
@@ -642,13 +658,14 @@ int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hi
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
         if (int e = set_lds(k_grow_inv<BM, TWG>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_inv<BM, TWG>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))), dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_grow_inv<BM, TWG>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))),
+                           dim3(gen_threads("ADMM_GROW_NT")), lds, s, a);
         return launch_check("k_grow_inv");
     });
 }
 template <int MODE, int BM, bool TWG> int gcol_launch(const GColArgs& a, size_t lds, dim3 grid, hipStream_t s) {
     if (int e = set_lds(k_gcol<MODE, BM, TWG>, lds)) return e;
-    hipLaunchKernelGGL((k_gcol<MODE, BM, TWG>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_gcol<MODE, BM, TWG>), grid, dim3(gen_threads("ADMM_GCOL_NT")), lds, s, a);
     return launch_check("k_gcol");
 }
 int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H, int W, long long P, int mode,
