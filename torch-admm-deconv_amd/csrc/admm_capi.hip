@@ -139,7 +139,9 @@ Layout make_layout(const admm_tv_desc& d) {
     L.rimg = L.gen ? take(img) : 0;
     for (int i = 0; i < 4; ++i) L.u[i] = take(img);
     L.b = k > 0 ? take(img_m) : 0;  // b = H_t(xin) is shared by the modules
-    L.fcT = take(G * (N + 1) * H * sizeof(float));  // one Wiener factor per module (its rho)
+    // one Wiener factor per module (its rho); on the fused path followed by their packed copies for
+    // the column pass (k_fc_pack)
+    L.fcT = take(G * (N + 1) * H * sizeof(float) * (L.gen ? 1 : 2));
     L.mT = take((N + 1) * H * sizeof(cf));
     // twiddles; on the generic path followed by the plan's Bluestein tables (make_plan)
     L.twW = take((W + (L.gen ? make_plan((int)W).ntab : 0)) * sizeof(cf));
@@ -284,6 +286,9 @@ template <class F> int with_row(int N, F&& f) {
 // column-pass tile order (k_pass_b pb_tile): planes per group, 1 = plane-major.  Two planes at
 // H >= 1024 (C3 pass B 0.376 -> 0.362 ms, C3 iso 0.381 -> 0.369; 4 and 8 planes slower: DRAM
 // locality), plane-major below (C2: neutral).  A/B knob ADMM_PASSB_GROUP.
+// values per lane of the column transforms (RowCfg<H>::E)
+int col_e(int H) { return H >= 1024 ? 16 : H >= 64 ? 8 : 4; }
+
 int passb_order(int H) { return std::max(1, std::min(64, env_int("ADMM_PASSB_GROUP", H >= 1024 ? 2 : 1))); }
 
 template <int H, int C> int pass_b_hc(const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N,
@@ -292,18 +297,19 @@ template <int H, int C> int pass_b_hc(const cf* spec, cf* out, const float* fcT,
     const int colblocks = N / C;
     const dim3 grid((unsigned)((long long)P * colblocks));
     const int order = passb_order(H);
+    const int fpack = mode == 0 && env_int("ADMM_PASSB_FPACK", 1) ? 1 : 0;  // A/B knob
     if (mode == 0) {
         if (int e = set_lds(k_pass_b<H, C, 0>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
-                           order);
+                           order, fpack);
     } else if (mode == 1) {
         if (int e = set_lds(k_pass_b<H, C, 1>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
-                           order);
+                           order, fpack);
     } else {
         if (int e = set_lds(k_pass_b<H, C, 2>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
-                           order);
+                           order, fpack);
     }
     return launch_check("k_pass_b");
 }
@@ -319,7 +325,7 @@ template <int H> int pass_b_h(const cf* spec, cf* out, const float* fcT, const c
             const int colblocks = N / 16;
             if (int e = set_lds(k_pass_b2<H, 8>, G::lds_bytes())) return e;
             hipLaunchKernelGGL((k_pass_b2<H, 8>), dim3((unsigned)((long long)P * colblocks)), dim3(G::NT), G::lds_bytes(),
-                               s, spec, out, fcT, twH, N, colblocks, ppm, passb_order(H));
+                               s, spec, out, fcT, twH, N, colblocks, ppm, passb_order(H), env_int("ADMM_PASSB_FPACK", 1) ? 1 : 0);
             return launch_check("k_pass_b2");
         }
         int C = env_int("ADMM_PASSB_C", 8);
@@ -443,6 +449,12 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
                                at<double2>(ws, Lo.twHd), rho + g, at<float>(ws, Lo.fcT) + (size_t)g * n, at<cf>(ws, Lo.mT),
                                k, H, N, W, Lo.sigma ? at<double2>(ws, Lo.sigma) : nullptr, spectra_scale(H, W));
             if (int e = launch_check("k_spectra")) return e;
+            if (!Lo.gen) {
+                float* fc = at<float>(ws, Lo.fcT) + (size_t)g * n;
+                hipLaunchKernelGGL(k_fc_pack, dim3((n + nt - 1) / nt), dim3(nt), 0, s, fc,
+                                   fc + (size_t)ngroups_of(d) * n, H, N, col_e(H));
+                if (int e = launch_check("k_fc_pack")) return e;
+            }
         }
     }
     return 0;

@@ -245,6 +245,15 @@ template <int H, int C> struct ColGeom {
     static constexpr size_t lds_bytes() { return sizeof(cf) * (H + (size_t)H * C); }
 };
 
+// Packed copy of one module's Wiener factors for the column pass: fcP[(kx L + t) E + j] =
+// fcT[kx H + t + L j] (the E factors a column-pass thread multiplies, contiguous)
+__global__ void k_fc_pack(const float* __restrict__ fcT, float* __restrict__ fcP, int H, int N, int E) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (N + 1) * H) return;
+    const int L = H / E, kx = i / H, r = i % H, t = r / E, j = r % E;
+    fcP[i] = fcT[(size_t)kx * H + t + L * j];
+}
+
 // XCD-aware remap (T1): blocks are dealt round-robin over the 8 XCDs; give each XCD a
 // contiguous range of logical ids so neighbouring column blocks (which share 128-B
 // lines of every row) run on the same L2 at about the same time.  Bijective for any nb.
@@ -281,7 +290,7 @@ __device__ __forceinline__ void pb_tile(unsigned lb, int colblocks, int order, b
 template <int H, int C, int MODE>
 __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCfg<H>::E), sizeof(cf) * (H + (size_t)H * C)))
     k_pass_b(const cf* spec_in, cf* spec_out, const float* __restrict__ fcT, const cf* __restrict__ mT,
-             const cf* __restrict__ twH_g, int N, int colblocks, int ppm, int order) {
+             const cf* __restrict__ twH_g, int N, int colblocks, int ppm, int order, int fpack) {
     using G = ColGeom<H, C>;
     constexpr int E = G::E, L = G::L;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -305,7 +314,22 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
     // multipliers for this column, prefetched with the data (L2-resident tables)
     using MT = typename std::conditional<MODE == 0, float, cf>::type;
     MT m[E];
-    {
+    if (MODE == 0 && fpack) {
+        // the packed copy of the Wiener factors (k_fc_pack, after the G tables of this region): a
+        // thread's E factors are contiguous, E/4 16-byte loads instead of E 4-byte ones
+        const float* fcP = fcT + (size_t)(gridDim.x / colblocks / ppm) * (N + 1) * H;  // fcT: this module's
+        const float4* q = reinterpret_cast<const float4*>(fcP + ((size_t)col * L + t) * E);
+#pragma unroll
+        for (int j = 0; j < E / 4; ++j) {
+            const float4 f = q[j];
+            if constexpr (MODE == 0) {
+                m[4 * j] = f.x;
+                m[4 * j + 1] = f.y;
+                m[4 * j + 2] = f.z;
+                m[4 * j + 3] = f.w;
+            }
+        }
+    } else {
         const rsrc_t rm = MODE == 0 ? make_rsrc(fcT, (unsigned)((size_t)(N + 1) * H * sizeof(float)))
                                     : make_rsrc(mT, (unsigned)((size_t)(N + 1) * H * sizeof(cf)));
         const int mo = (col * H + t) * (int)sizeof(MT);
@@ -372,7 +396,7 @@ __device__ __forceinline__ void bstore_f4(rsrc_t r, int voff, int soff, float4 v
 template <int H, int CP>
 __global__ void __launch_bounds__(CP * (H / RowCfg<H>::E), PASSB2_MINW)
     k_pass_b2(const cf* spec_in, cf* spec_out, const float* __restrict__ fcT, const cf* __restrict__ twH_g, int N,
-              int colblocks, int ppm, int order) {
+              int colblocks, int ppm, int order, int fpack) {
     using G = ColGeom<H, CP>;
     constexpr int E = G::E, L = G::L;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -400,9 +424,26 @@ __global__ void __launch_bounds__(CP * (H / RowCfg<H>::E), PASSB2_MINW)
     // after the first column is done, to keep the register footprint at one set
     const rsrc_t rm = make_rsrc(fcT, (unsigned)((size_t)(N + 1) * H * sizeof(float)));
     const int mo = (col * H + t) * (int)sizeof(float);
-    float m0[E], m1[E];
+    // packed Wiener factors (k_fc_pack): a thread's E factors of a column are contiguous
+    const float* fcP = fcT + (size_t)(gridDim.x / colblocks / ppm) * (N + 1) * H;  // fcT: this module's
+    auto packed = [&](int c, float (&m)[E]) {
+        const float4* q = reinterpret_cast<const float4*>(fcP + ((size_t)c * L + t) * E);
 #pragma unroll
-    for (int j = 0; j < E; ++j) m0[j] = bload_f(rm, mo, j * L * (int)sizeof(float));
+        for (int j = 0; j < E / 4; ++j) {
+            const float4 f = q[j];
+            m[4 * j] = f.x;
+            m[4 * j + 1] = f.y;
+            m[4 * j + 2] = f.z;
+            m[4 * j + 3] = f.w;
+        }
+    };
+    float m0[E], m1[E];
+    if (fpack) {
+        packed(col, m0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) m0[j] = bload_f(rm, mo, j * L * (int)sizeof(float));
+    }
     __syncthreads();
     ColBuf<CP> buf{data + cp};
     fft<H, L, -1, 1, 1>(v0, buf, tw, t);
@@ -427,8 +468,12 @@ __global__ void __launch_bounds__(CP * (H / RowCfg<H>::E), PASSB2_MINW)
         for (int j = 0; j < E; ++j) v0[j] = cscale(v0[j], m0[j]);
     }
     fft<H, L, +1, 1, 1>(v0, buf, tw, t);
+    if (fpack) {
+        packed(col + 1, m1);
+    } else {
 #pragma unroll
-    for (int j = 0; j < E; ++j) m1[j] = bload_f(rm, mo + H * (int)sizeof(float), j * L * (int)sizeof(float));
+        for (int j = 0; j < E; ++j) m1[j] = bload_f(rm, mo + H * (int)sizeof(float), j * L * (int)sizeof(float));
+    }
     fft<H, L, -1, 1, 1>(v1, buf, tw, t);
 #pragma unroll
     for (int j = 0; j < E; ++j) v1[j] = cscale(v1[j], m1[j]);
