@@ -393,6 +393,57 @@ __global__ void __launch_bounds__(TPB) k_colmimic_mix(const cf* __restrict__ si,
     }
 }
 
+
+// pass A mimic with the u_x, u_y, b streams moved as 16-byte accesses (lane t holds pixel pairs
+// 2t, 2t+1 + 128 j): half the load/store instructions for those streams
+template <int R>
+__global__ void __launch_bounds__(256) k_mimic_u4(const cf* __restrict__ sp, const cf* __restrict__ uxi,
+                                                  const cf* __restrict__ uyi, const cf* __restrict__ b,
+                                                  cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
+                                                  int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    cf acc[E];
+    for (int j = 0; j < E; ++j) acc[j] = ld(&sp[base + (size_t)((i0 - 1 + H) & (H - 1)) * N + t + L * j], true);
+    for (int rr = 0; rr <= R; ++rr) {
+        const size_t ro = base + (size_t)((i0 + rr) & (H - 1)) * N;
+        const size_t rm = base + (size_t)((i0 + rr - 1 + H) & (H - 1)) * N;
+        cf x[E];
+        for (int j = 0; j < E; ++j) x[j] = ld(&sp[ro + t + L * j], true);
+        const f4* uy4 = reinterpret_cast<const f4*>(uyi + ro);
+        f4* uyo4 = reinterpret_cast<f4*>(uyo + ro);
+        const f4* ux4 = reinterpret_cast<const f4*>(uxi + ro);
+        f4* uxo4 = reinterpret_cast<f4*>(uxo + ro);
+        const f4* b4 = reinterpret_cast<const f4*>(b + rm);
+        for (int j = 0; j < E / 2; ++j) {
+            f4 u = __builtin_nontemporal_load(&uy4[t + L * j]);
+            u.x += x[2 * j].x; u.y += acc[2 * j].y; u.z += x[2 * j + 1].x; u.w += acc[2 * j + 1].y;
+            if (rr < R) __builtin_nontemporal_store(u, &uyo4[t + L * j]);
+        }
+        if (rr >= 1) {
+            for (int j = 0; j < E / 2; ++j) {
+                f4 bb = __builtin_nontemporal_load(&b4[t + L * j]);
+                acc[2 * j].x += bb.x; acc[2 * j].y -= bb.y; acc[2 * j + 1].x += bb.z; acc[2 * j + 1].y -= bb.w;
+            }
+            for (int j = 0; j < E; ++j) st(&so[rm + t + L * j], acc[j], true);
+        }
+        if (rr < R) {
+            for (int j = 0; j < E / 2; ++j) {
+                f4 u = __builtin_nontemporal_load(&ux4[t + L * j]);
+                u.x -= x[2 * j].y; u.y += x[2 * j].x; u.z -= x[2 * j + 1].y; u.w += x[2 * j + 1].x;
+                __builtin_nontemporal_store(u, &uxo4[t + L * j]);
+            }
+        }
+        for (int j = 0; j < E; ++j) acc[j] = x[j];
+    }
+}
+
 int main() {
     const int P = 192, H = 1024;
     const size_t n = (size_t)P * H * N;  // cf per array
@@ -418,6 +469,14 @@ int main() {
         printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
     const double arr = (double)n * sizeof(cf);
+    if (getenv("U4_SWEEP")) {
+        const long long ns = (long long)P * H / 8;
+        for (int rep = 0; rep < 3; ++rep) {
+            timeit("A row-major nt (prod) R=8", 7 * arr, [&] { k_mimic<8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A u/b streams 16 B/lane R=8", 7 * arr, [&] { k_mimic_u4<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+        }
+        return 0;
+    }
     if (getenv("MIXED_SWEEP3")) {  // T = 2 row-pair tiles: pass B reads whole 128-B lines
         const long long ns = (long long)P * H / 8;
         const int colblocks = N / 8;

@@ -138,7 +138,9 @@ Layout make_layout(const admm_tv_desc& d) {
     L.spec[1] = take(img);
     L.rimg = L.gen ? take(img) : 0;
     for (int i = 0; i < 4; ++i) L.u[i] = take(img);
-    L.b = k > 0 ? take(img_m) : 0;  // b = H_t(xin) is shared by the modules
+    // b = H_t(xin), shared by the modules; on the fused path also without a PSF (b = xin re-laid
+    // out for the inference pass, lane-paired rows)
+    L.b = (k > 0 || !L.gen) ? take(img_m) : 0;
     // one Wiener factor per module (its rho); on the fused path followed by their packed copies for
     // the column pass (k_fc_pack)
     L.fcT = take(G * (N + 1) * H * sizeof(float) * (L.gen ? 1 : 2));
@@ -204,40 +206,64 @@ template <int N> struct RowOps {
     using G = RowKernelGeom<N>;
     static unsigned blocks(long long items) { return (unsigned)((items + G::SG - 1) / G::SG); }
 
-    static int r2c(const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s) {
-        hipLaunchKernelGGL(k_row_r2c<N>, dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, img, spec, twW, rows);
+    // pl: the lane-paired row layout (admm_kernels.hpp ld_row) for the image side
+    static int r2c(const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s, bool pl = false) {
+        if (pl)
+            hipLaunchKernelGGL((k_row_r2c<N, true>), dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, img, spec, twW, rows);
+        else
+            hipLaunchKernelGGL((k_row_r2c<N, false>), dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, img, spec, twW, rows);
         return launch_check("k_row_r2c");
     }
-    static int c2r(const cf* spec, float* img, const cf* twW, long long rows, hipStream_t s) {
-        hipLaunchKernelGGL(k_row_c2r<N>, dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, spec, img, twW, rows);
+    static int c2r(const cf* spec, float* img, const cf* twW, long long rows, hipStream_t s, bool pl = false) {
+        if (pl)
+            hipLaunchKernelGGL((k_row_c2r<N, true>), dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, spec, img, twW, rows);
+        else
+            hipLaunchKernelGGL((k_row_c2r<N, false>), dim3(blocks(rows)), dim3(G::NT), G::lds_bytes(), s, spec, img, twW, rows);
         return launch_check("k_row_c2r");
     }
-    template <bool ISO, bool FIRST, bool HIST> static void pa(const PassAArgs& a, unsigned nb, hipStream_t s) {
-        hipLaunchKernelGGL((k_pass_a<N, ISO, FIRST, HIST>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+    static int pair(const float* img, float* out, long long rows, hipStream_t s) {
+        hipLaunchKernelGGL(k_row_pair<N>, dim3(blocks(rows)), dim3(G::NT), 0, s, img, out, rows);
+        return launch_check("k_row_pair");
     }
-    static int pass_a(const PassAArgs& a, bool iso, bool first, bool hist, hipStream_t s) {
+    template <bool ISO, bool FIRST, bool HIST, bool PL> static void pa(const PassAArgs& a, unsigned nb, hipStream_t s) {
+        hipLaunchKernelGGL((k_pass_a<N, ISO, FIRST, HIST, PL>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+    }
+    static int pass_a(const PassAArgs& a, bool iso, bool first, bool hist, hipStream_t s, bool pl = false) {
         const unsigned nb = blocks(a.nstrips);
         const int sel = (iso ? 4 : 0) | (first ? 2 : 0) | (hist ? 1 : 0);
+        if (pl && !hist) {  // inference: lane-paired images
+            switch (sel) {
+                case 0: pa<false, false, false, true>(a, nb, s); break;
+                case 2: pa<false, true, false, true>(a, nb, s); break;
+                case 4: pa<true, false, false, true>(a, nb, s); break;
+                default: pa<true, true, false, true>(a, nb, s); break;
+            }
+            return launch_check("k_pass_a");
+        }
         switch (sel) {
-            case 0: pa<false, false, false>(a, nb, s); break;
-            case 1: pa<false, false, true>(a, nb, s); break;
-            case 2: pa<false, true, false>(a, nb, s); break;
-            case 3: pa<false, true, true>(a, nb, s); break;
-            case 4: pa<true, false, false>(a, nb, s); break;
-            case 5: pa<true, false, true>(a, nb, s); break;
-            case 6: pa<true, true, false>(a, nb, s); break;
-            default: pa<true, true, true>(a, nb, s); break;
+            case 0: pa<false, false, false, false>(a, nb, s); break;
+            case 1: pa<false, false, true, false>(a, nb, s); break;
+            case 2: pa<false, true, false, false>(a, nb, s); break;
+            case 3: pa<false, true, true, false>(a, nb, s); break;
+            case 4: pa<true, false, false, false>(a, nb, s); break;
+            case 5: pa<true, false, true, false>(a, nb, s); break;
+            case 6: pa<true, true, false, false>(a, nb, s); break;
+            default: pa<true, true, true, false>(a, nb, s); break;
         }
         return launch_check("k_pass_a");
     }
-    static int iso_norm(const IsoArgs& a, bool first, bool hist, hipStream_t s) {
+    static int iso_norm(const IsoArgs& a, bool first, bool hist, hipStream_t s, bool pl = false) {
         const unsigned nb = blocks(a.nitems);
-        if (first)
-            hipLaunchKernelGGL((k_iso_norm<N, true, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        if (first && pl)
+            hipLaunchKernelGGL((k_iso_norm<N, true, false, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        else if (first)
+            hipLaunchKernelGGL((k_iso_norm<N, true, false, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         else if (hist)
-            hipLaunchKernelGGL((k_iso_norm<N, false, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+            hipLaunchKernelGGL((k_iso_norm<N, false, true, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        else if (pl)
+            hipLaunchKernelGGL((k_iso_norm<N, false, false, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         else
-            hipLaunchKernelGGL((k_iso_norm<N, false, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+            hipLaunchKernelGGL((k_iso_norm<N, false, false, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         return launch_check("k_iso_norm");
     }
     template <bool ISO, bool LASTK, bool FIRSTK> static void bpa(const BwdArgs& a, unsigned nb, hipStream_t s) {
@@ -488,7 +514,7 @@ int strip_rows(int H, int N, long long rows, bool aniso_fwd = false) {
 
 // b = H_t(xin) into `bb` through the FFT passes (scratch: spec)
 int psf_transpose_into(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* xin, float* bb, cf* spec,
-                       int mode, hipStream_t s) {
+                       int mode, hipStream_t s, bool pl = false) {
     const long long rows = d.B * d.C * d.H;
     const int H = (int)d.H, N = (int)d.W / 2;
     cf* twW = at<cf>(ws, Lo.twW);
@@ -496,7 +522,7 @@ int psf_transpose_into(const admm_tv_desc& d, const Layout& Lo, void* ws, const 
     if (e) return e;
     if ((e = pass_b(H, spec, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), at<cf>(ws, Lo.twH), N, (int)(d.B * d.C), mode, s)))
         return e;
-    return with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec, bb, twW, rows, s); });
+    return with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec, bb, twW, rows, s, pl); });
 }
 
 
@@ -905,18 +931,28 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         return reinterpret_cast<cf*>(static_cast<char*>(hist) + Hs.t_off + (size_t)(k - 1) * Hs.t_slot);
     };
 
+    // The inference path keeps its internal images (u, b, iso norm maps) in the lane-paired row
+    // layout (16-byte accesses, admm_kernels.hpp ld_row); the training history stays in pixel order.
+    // ADMM_PL=0 for the pixel-order layout (A/B).
+    const bool pl = !train && env_int("ADMM_PL", 1) != 0;
+
     // b = H_t(xin) once (the reference recomputes it every iteration, deconv.py:104)
     const float* bimg = xin;
     if (d.kh > 0) {
         ProfScope ps(3, s);
         float* bb = at<float>(ws, Lo.b);
-        if (int e = psf_transpose_into(d, Lo, ws, xin, bb, spec[0], 1, s)) return e;
+        if (int e = psf_transpose_into(d, Lo, ws, xin, bb, spec[0], 1, s, pl)) return e;
+        bimg = bb;
+    } else if (pl) {  // b = xin, re-laid out
+        ProfScope ps(3, s);
+        float* bb = at<float>(ws, Lo.b);
+        if (int e = with_row(N, [&](auto ops) { return decltype(ops)::pair(xin, bb, Pm * H, s); })) return e;
         bimg = bb;
     }
     for (int g = 0; g < G; ++g) {  // r_1 = b for every module
         ProfScope ps(3, s);
         cf* t0 = (keep_t ? ht(1) : spec[0]) + (size_t)g * Pm * H * N;
-        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, t0, twW, Pm * H, s); });
+        int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, t0, twW, Pm * H, s, pl); });
         if (e) return e;
     }
     const int R = strip_rows(H, N, rows, !d.iso && !hist);
@@ -956,7 +992,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
             float* nout = train ? hn(it) : at<float>(ws, Lo.nsq);
             IsoArgs ia{spec[cur], uxi, uyi, nprev, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
                        (long long)Lo.ngroups * H, Pm};
-            int e = with_row(N, [&](auto ops) { return decltype(ops)::iso_norm(ia, first, train, s); });
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::iso_norm(ia, first, train, s, pl); });
             if (e) return e;
             const long long n4 = 2LL * H * W / 4;
             const int gpm = Lo.ngroups / G;  // plane groups per module
@@ -974,7 +1010,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
             ProfScope ps(0, s);
             cf* tout = (keep_t && it < d.maxit) ? ht(it + 1) : spec[1 - cur];
             PassAArgs pa{spec[cur], tout, bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, rows / R, Pm};
-            int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, train, s); });
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, train, s, pl); });
             if (e) return e;
         }
         cur = 1 - cur;

@@ -180,8 +180,49 @@ __device__ __forceinline__ void load_tw(cf* dst, const cf* __restrict__ src, int
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
+// ---------------------------------------------------------------------------
+// Row layouts of the internal images (u_x, u_y, b, iso norm maps).  A sub-group lane t holds the
+// pixel pairs t + L j (j < E) of a row ("natural layout").  PL = false stores them in pixel
+// order (8-byte accesses, one per pair).  PL = true ("lane-paired") stores the two pairs a lane
+// handles in consecutive registers 2j', 2j'+1 next to each other: float4 slot t + L j' of the row
+// holds pairs t + 2j' L and t + (2j'+1) L, so every such stream moves 16 bytes per lane and
+// instruction (half the instructions; pass A's access pattern: 1.014 -> 0.955 ms in
+// tools/membench/stream_mimic U4_SWEEP).  A pure permutation inside each row: used for the
+// workspace images of the inference path, never for the caller's tensors or the training history.
+// ---------------------------------------------------------------------------
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int E, int L, bool PL, bool NT> __device__ __forceinline__ void ld_row(const cf* row, int t, cf (&v)[E]) {
+    if constexpr (PL) {
+        static_assert(E % 2 == 0, "lane-paired rows need an even number of values per lane");
+        const f4v* r4 = reinterpret_cast<const f4v*>(row);
+#pragma unroll
+        for (int j = 0; j < E / 2; ++j) {
+            const f4v q = NT ? __builtin_nontemporal_load(&r4[t + L * j]) : r4[t + L * j];
+            v[2 * j] = mkc(q.x, q.y);
+            v[2 * j + 1] = mkc(q.z, q.w);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) v[j] = ld_pol<NT>(&row[t + L * j]);
+    }
+}
+template <int E, int L, bool PL, bool NT> __device__ __forceinline__ void st_row(cf* row, int t, const cf (&v)[E]) {
+    if constexpr (PL) {
+        f4v* r4 = reinterpret_cast<f4v*>(row);
+#pragma unroll
+        for (int j = 0; j < E / 2; ++j) {
+            const f4v q = {v[2 * j].x, v[2 * j].y, v[2 * j + 1].x, v[2 * j + 1].y};
+            if constexpr (NT) __builtin_nontemporal_store(q, &r4[t + L * j]);
+            else r4[t + L * j] = q;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) st_pol<NT>(&row[t + L * j], v[j]);
+    }
+}
+
 // real rows -> packed row spectra
-template <int N>
+template <int N, bool PL>
 __global__ void __launch_bounds__(256) k_row_r2c(const float* __restrict__ img, cf* __restrict__ spec,
                                                  const cf* __restrict__ twW_g, long long rows) {
     using G = RowKernelGeom<N>;
@@ -196,8 +237,7 @@ __global__ void __launch_bounds__(256) k_row_r2c(const float* __restrict__ img, 
     RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
     const cf* src = reinterpret_cast<const cf*>(img + row * G::W);
     cf v[E];
-#pragma unroll
-    for (int j = 0; j < E; ++j) v[j] = src[t + L * j];
+    ld_row<E, L, PL, false>(src, t, v);
     RowXf<N>::r2c(v, buf, tw, t);
     cf* dst = spec + row * N;
 #pragma unroll
@@ -205,7 +245,7 @@ __global__ void __launch_bounds__(256) k_row_r2c(const float* __restrict__ img, 
 }
 
 // packed row spectra -> real rows
-template <int N>
+template <int N, bool PL>
 __global__ void __launch_bounds__(256) k_row_c2r(const cf* __restrict__ spec, float* __restrict__ img,
                                                  const cf* __restrict__ twW_g, long long rows) {
     using G = RowKernelGeom<N>;
@@ -224,8 +264,20 @@ __global__ void __launch_bounds__(256) k_row_c2r(const cf* __restrict__ spec, fl
     for (int j = 0; j < E; ++j) v[j] = src[t + L * j];
     RowXf<N>::c2r(v, buf, tw, t);
     cf* dst = reinterpret_cast<cf*>(img + row * G::W);
-#pragma unroll
-    for (int j = 0; j < E; ++j) dst[t + L * j] = v[j];
+    st_row<E, L, PL, false>(dst, t, v);
+}
+
+// real rows in pixel order -> the lane-paired layout (b = xin on the inference path without a PSF)
+template <int N>
+__global__ void __launch_bounds__(256) k_row_pair(const float* __restrict__ img, float* __restrict__ out, long long rows) {
+    using G = RowKernelGeom<N>;
+    constexpr int E = G::E, L = G::L;
+    const int sgl = threadIdx.x / L, t = threadIdx.x % L;
+    const long long row = (long long)blockIdx.x * G::SG + sgl;
+    if (row >= rows) return;
+    cf v[E];
+    ld_row<E, L, false, true>(reinterpret_cast<const cf*>(img + row * G::W), t, v);
+    st_row<E, L, true, false>(reinterpret_cast<cf*>(out + row * G::W), t, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -540,8 +592,9 @@ __device__ __forceinline__ cf prev_u(const cf* __restrict__ src, const cf* __res
     }
 }
 
-template <int N, bool ISO, bool FIRST, bool HIST>
+template <int N, bool ISO, bool FIRST, bool HIST, bool PL>
 __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
+    static_assert(!(PL && HIST), "the training history keeps the pixel-order layout");
     using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
     constexpr bool kSpecNT = (ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512);
@@ -600,10 +653,20 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
         cf wyc[E];
         {
             cf uy[E], fy[E];
+            if constexpr (PL) {
+                if constexpr (FIRST) {
 #pragma unroll
-            for (int j = 0; j < E; ++j) {
-                uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
-                if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
+                    for (int j = 0; j < E; ++j) uy[j] = mkc(0.f, 0.f);
+                } else {
+                    ld_row<E, L, true, (ADMM_NT & 16) != 0>(uyi + ro, t, uy);
+                }
+                if constexpr (ISO) ld_row<E, L, true, false>(nsy + ro, t, fy);
+            } else {
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    uy[j] = prev_u<ISO, FIRST, HIST>(uyi, npy, ro + t + L * j, tau);
+                    if constexpr (ISO) fy[j] = nsy[ro + t + L * j];
+                }
             }
 #pragma unroll
             for (int j = 0; j < E; ++j) {
@@ -616,8 +679,12 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
                 wyc[j] = mkc(z0 - n0, z1 - n1);
             }
             if (rr < R) {
+                if constexpr (PL) {
+                    st_row<E, L, true, (ADMM_NT & 1) != 0>(uyo + ro, t, uy);
+                } else {
 #pragma unroll
-                for (int j = 0; j < E; ++j) sta(&uyo[ro + t + L * j], uy[j]);
+                    for (int j = 0; j < E; ++j) sta(&uyo[ro + t + L * j], uy[j]);
+                }
             }
         }
 
@@ -625,13 +692,14 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
         if (rr >= 1) {
             const int gm = (g - 1 + H) & (H - 1);
             const size_t rm = (size_t)gm * N;
-            cf r[E], sh[E];
+            cf r[E], sh[E], bv[E];
+            if constexpr (PL) ld_row<E, L, true, (ADMM_NT & 16) != 0>(bimg + rm, t, bv);
 #pragma unroll
             for (int j = 0; j < E; ++j) sh[j].x = __shfl(wxp[j].x, (t + 1) & (L - 1), L);
 #pragma unroll
             for (int j = 0; j < E; ++j) {
                 const float wr = (t == L - 1) ? sh[(j + 1) & (E - 1)].x : sh[j].x;  // w_x at pixel q1+1
-                const cf bb = lda<16>(&bimg[rm + t + L * j]);
+                const cf bb = PL ? bv[j] : lda<16>(&bimg[rm + t + L * j]);
                 const float v0 = (wxp[j].x - wxp[j].y) + (wyp[j].x - wyc[j].x);
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
                 r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
@@ -644,10 +712,21 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
         // ---- x direction: a_x = x[g][j] - x[g][j-1] + u_x; z_x, u_x, w_x of row g
         if (rr < R) {
             cf ux[E], fx[E], sh[E];
+            if constexpr (PL) {
+                if constexpr (FIRST) {
+#pragma unroll
+                    for (int j = 0; j < E; ++j) ux[j] = mkc(0.f, 0.f);
+                } else {
+                    ld_row<E, L, true, (ADMM_NT & 16) != 0>(uxi + ro, t, ux);
+                }
+                if constexpr (ISO) ld_row<E, L, true, false>(nsx + ro, t, fx);
+            }
 #pragma unroll
             for (int j = 0; j < E; ++j) {
-                ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
-                if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
+                if constexpr (!PL) {
+                    ux[j] = prev_u<ISO, FIRST, HIST>(uxi, npx, ro + t + L * j, tau);
+                    if constexpr (ISO) fx[j] = nsx[ro + t + L * j];
+                }
                 sh[j].x = __shfl(xcur[j].y, (t - 1) & (L - 1), L);
             }
 #pragma unroll
@@ -661,8 +740,12 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
                 ux[j] = HIST ? mkc(a0, a1) : mkc(n0, n1);
                 wxp[j] = mkc(z0 - n0, z1 - n1);
             }
+            if constexpr (PL) {
+                st_row<E, L, true, (ADMM_NT & 1) != 0>(uxo + ro, t, ux);
+            } else {
 #pragma unroll
-            for (int j = 0; j < E; ++j) sta(&uxo[ro + t + L * j], ux[j]);
+                for (int j = 0; j < E; ++j) sta(&uxo[ro + t + L * j], ux[j]);
+            }
         }
 #pragma unroll
         for (int j = 0; j < E; ++j) {
@@ -690,8 +773,9 @@ struct IsoArgs {
     long long ppm;     // planes per module (see PassAArgs)
 };
 
-template <int N, bool FIRST, bool HIST>
+template <int N, bool FIRST, bool HIST, bool PL>
 __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
+    static_assert(!(PL && HIST), "the training history keeps the pixel-order layout");
     using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -729,7 +813,11 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
         const size_t rn = (size_t)g * N;                      // norm maps are per pixel, shared by planes
         const cf* uxi = reinterpret_cast<const cf*>(a.uxi);
         const cf* uyi = reinterpret_cast<const cf*>(a.uyi);
-        cf sh[E];
+        cf sh[E], uxv[E], uyv[E];
+        if constexpr (PL && !FIRST) {
+            ld_row<E, L, true, false>(uxi + ro, t, uxv);
+            ld_row<E, L, true, false>(uyi + ro, t, uyv);
+        }
 #pragma unroll
         for (int j = 0; j < E; ++j) sh[j].x = __shfl(xc[j].y, (t - 1) & (L - 1), L);
 #pragma unroll
@@ -737,6 +825,9 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
             cf ux, uy;
             if constexpr (FIRST) {
                 ux = uy = mkc(0.f, 0.f);
+            } else if constexpr (PL) {
+                ux = uxv[j];
+                uy = uyv[j];
             } else if constexpr (HIST) {
                 const cf ax = uxi[ro + t + L * j], ay = uyi[ro + t + L * j];
                 const cf nx = npx[rn + t + L * j], ny = npy[rn + t + L * j];
@@ -757,11 +848,8 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
     }
     cf* px = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 0) * H * W) + (size_t)g * N;
     cf* py = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 1) * H * W) + (size_t)g * N;
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        px[t + L * j] = sx[j];
-        py[t + L * j] = sy[j];
-    }
+    st_row<E, L, PL, false>(px, t, sx);  // the norm maps take the layout of u (pass A reads both alike)
+    st_row<E, L, PL, false>(py, t, sy);
 }
 
 // nsq[k] = sum_g partial[g][k], k over 2*H*W, fixed order (deterministic)
