@@ -444,6 +444,61 @@ __global__ void __launch_bounds__(256) k_mimic_u4(const cf* __restrict__ sp, con
     }
 }
 
+
+// all seven streams of pass A at 16 bytes per lane (spectrum too): lane t holds pairs 2t, 2t+1 + 128 j
+template <int R>
+__global__ void __launch_bounds__(256) k_mimic_all16(const cf* __restrict__ sp, const cf* __restrict__ uxi,
+                                                     const cf* __restrict__ uyi, const cf* __restrict__ b,
+                                                     cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
+                                                     int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    f4 acc[E / 2];
+    {
+        const f4* s4 = reinterpret_cast<const f4*>(sp + base + (size_t)((i0 - 1 + H) & (H - 1)) * N);
+        for (int j = 0; j < E / 2; ++j) acc[j] = __builtin_nontemporal_load(&s4[t + L * j]);
+    }
+    for (int rr = 0; rr <= R; ++rr) {
+        const size_t ro = base + (size_t)((i0 + rr) & (H - 1)) * N;
+        const size_t rm = base + (size_t)((i0 + rr - 1 + H) & (H - 1)) * N;
+        f4 x[E / 2];
+        const f4* s4 = reinterpret_cast<const f4*>(sp + ro);
+        for (int j = 0; j < E / 2; ++j) x[j] = __builtin_nontemporal_load(&s4[t + L * j]);
+        const f4* uy4 = reinterpret_cast<const f4*>(uyi + ro);
+        f4* uyo4 = reinterpret_cast<f4*>(uyo + ro);
+        const f4* ux4 = reinterpret_cast<const f4*>(uxi + ro);
+        f4* uxo4 = reinterpret_cast<f4*>(uxo + ro);
+        const f4* b4 = reinterpret_cast<const f4*>(b + rm);
+        f4* so4 = reinterpret_cast<f4*>(so + rm);
+        for (int j = 0; j < E / 2; ++j) {
+            f4 u = __builtin_nontemporal_load(&uy4[t + L * j]);
+            u += x[j] - acc[j];
+            if (rr < R) __builtin_nontemporal_store(u, &uyo4[t + L * j]);
+        }
+        if (rr >= 1) {
+            for (int j = 0; j < E / 2; ++j) {
+                f4 bb = __builtin_nontemporal_load(&b4[t + L * j]);
+                acc[j] += bb;
+                __builtin_nontemporal_store(acc[j], &so4[t + L * j]);
+            }
+        }
+        if (rr < R) {
+            for (int j = 0; j < E / 2; ++j) {
+                f4 u = __builtin_nontemporal_load(&ux4[t + L * j]);
+                u -= x[j];
+                __builtin_nontemporal_store(u, &uxo4[t + L * j]);
+            }
+        }
+        for (int j = 0; j < E / 2; ++j) acc[j] = x[j];
+    }
+}
+
 int main() {
     const int P = 192, H = 1024;
     const size_t n = (size_t)P * H * N;  // cf per array
@@ -474,6 +529,7 @@ int main() {
         for (int rep = 0; rep < 3; ++rep) {
             timeit("A row-major nt (prod) R=8", 7 * arr, [&] { k_mimic<8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
             timeit("A u/b streams 16 B/lane R=8", 7 * arr, [&] { k_mimic_u4<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A all streams 16 B/lane R=8", 7 * arr, [&] { k_mimic_all16<8><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
         }
         return 0;
     }
