@@ -35,6 +35,8 @@ def main():
     shapes = SHAPES
     if os.environ.get("SHAPES"):  # e.g. SHAPES=0,4 (indices into SHAPES)
         shapes = [SHAPES[int(i)] for i in os.environ["SHAPES"].split(",")]
+    if os.environ.get("SHAPE_LIST"):  # e.g. SHAPE_LIST=1x3x1024x1024,3x3x1024x1024
+        shapes = [tuple(int(d) for d in s.split("x")) for s in os.environ["SHAPE_LIST"].split(",")]
     for B, C, H, W in shapes:
         x = blurred_batch(B, C, H, W, psf.cpu(), seed=1, device=dev)
         for st in settings:

@@ -512,6 +512,23 @@ int strip_rows(int H, int N, long long rows, bool aniso_fwd = false) {
     return R;
 }
 
+// the calling thread's auxiliary stream on the current device (created once, never destroyed)
+hipStream_t aux_stream() {
+    thread_local hipStream_t st[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (!st[dev] && hipStreamCreateWithFlags(&st[dev], hipStreamNonBlocking) != hipSuccess) st[dev] = nullptr;
+    return st[dev];
+}
+
+// planes per chunk of the aniso inference solve (run_forward): ADMM_CHUNK_PLANES > 0 sets it,
+// 0 (or >= P) solves all planes at once
+long long chunk_planes(int H, int W, long long P) {
+    (void)H; (void)W;
+    const long long c = env_int("ADMM_CHUNK_PLANES", 0);
+    return (c <= 0 || c >= P) ? P : c;
+}
+
 // b = H_t(xin) into `bb` through the FFT passes (scratch: spec)
 int psf_transpose_into(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* xin, float* bb, cf* spec,
                        int mode, hipStream_t s, bool pl = false) {
@@ -917,7 +934,6 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     cf* mT = at<cf>(ws, Lo.mT);
     cf* spec[2] = {at<cf>(ws, Lo.spec[0]), at<cf>(ws, Lo.spec[1])};
     float* u[4] = {at<float>(ws, Lo.u[0]), at<float>(ws, Lo.u[1]), at<float>(ws, Lo.u[2]), at<float>(ws, Lo.u[3])};
-    const long long rows = P * H;
     const bool train = hist != nullptr;
     const Hist Hs = make_hist(d);
     auto ha = [&](int k, int comp) -> float* {  // a_k image (k >= 1), comp 0 = x, 1 = y
@@ -955,19 +971,29 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, t0, twW, Pm * H, s, pl); });
         if (e) return e;
     }
-    const int R = strip_rows(H, N, rows, !d.iso && !hist);
+    // Planes [p0, p0 + np) through all iterations (ppm: planes per module of that range).  The
+    // aniso inference path solves independent planes, so it may run the iterations chunk by chunk:
+    // a chunk's spectra, u and b (28 B/px) then stay in the 256 MiB Infinity Cache between the
+    // passes instead of streaming through HBM (ADMM_CHUNK_PLANES).
+    auto solve_planes = [&](long long p0, long long np, long long ppm, hipStream_t st) -> int {
+    const size_t so = (size_t)p0 * H * N, io = (size_t)p0 * H * W;  // cf / float offsets
+    cf* cspec[2] = {spec[0] + so, spec[1] + so};
+    const long long crows = np * H;
+    const float* cb = bimg + io;
+    float* cout = out + io;
+    const int R = strip_rows(H, N, crows, !d.iso && !hist);
 
     int cur = 0, uin = 0;  // spec[cur] holds the current r spectra; u[2*uin], u[2*uin+1] = u_x, u_y in
     for (int it = 1; it <= d.maxit; ++it) {
         {
-            ProfScope ps(1, s);
+            ProfScope ps(1, st);
             // PSF-gradient training keeps r_k's spectrum: the column pass then runs out of place
-            const cf* tin = keep_t ? ht(it) : spec[cur];
-            if (int e = pass_b_oop(H, tin, spec[cur], fcT, mT, twH, N, (int)P, 0, s, (int)Pm)) return e;
+            const cf* tin = keep_t ? ht(it) : cspec[cur];
+            if (int e = pass_b_oop(H, tin, cspec[cur], fcT, mT, twH, N, (int)np, 0, st, (int)ppm)) return e;
         }
         if (it == d.maxit) {
-            ProfScope ps(3, s);
-            int e = with_row(N, [&](auto ops) { return decltype(ops)::c2r(spec[cur], out, twW, rows, s); });
+            ProfScope ps(3, st);
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::c2r(cspec[cur], cout, twW, crows, st); });
             if (e) return e;
             if (!train) break;
         }
@@ -981,41 +1007,66 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
             uyo = ha(it, 1);
             if (d.iso && !first) nprev = hn(it - 1);
         } else {
-            uxi = u[2 * uin];
-            uyi = u[2 * uin + 1];
-            uxo = u[2 * (1 - uin)];
-            uyo = u[2 * (1 - uin) + 1];
+            uxi = u[2 * uin] + io;
+            uyi = u[2 * uin + 1] + io;
+            uxo = u[2 * (1 - uin)] + io;
+            uyo = u[2 * (1 - uin) + 1] + io;
         }
         const float* nsq = nullptr;
         if (d.iso) {
-            ProfScope ps(2, s);
+            ProfScope ps(2, st);
             float* nout = train ? hn(it) : at<float>(ws, Lo.nsq);
-            IsoArgs ia{spec[cur], uxi, uyi, nprev, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
+            IsoArgs ia{cspec[cur], uxi, uyi, nprev, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
                        (long long)Lo.ngroups * H, Pm};
-            int e = with_row(N, [&](auto ops) { return decltype(ops)::iso_norm(ia, first, train, s, pl); });
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::iso_norm(ia, first, train, st, pl); });
             if (e) return e;
             const long long n4 = 2LL * H * W / 4;
             const int gpm = Lo.ngroups / G;  // plane groups per module
             for (int g = 0; g < G; ++g) {     // each module's norm over its own planes
-                hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st,
                                    at<float4>(ws, Lo.part) + (size_t)g * gpm * n4,  // n4 float4 = 2HW floats
                                    reinterpret_cast<float4*>(nout) + (size_t)g * n4, gpm, n4);
                 if ((e = launch_check("k_iso_reduce"))) return e;
             }
             // sharded batch: the per-pixel sums must cover every rank's planes
-            allreduce(d, nout, (size_t)G * 2 * H * W, s);
+            allreduce(d, nout, (size_t)G * 2 * H * W, st);
             nsq = nout;
         }
         {
-            ProfScope ps(0, s);
-            cf* tout = (keep_t && it < d.maxit) ? ht(it + 1) : spec[1 - cur];
-            PassAArgs pa{spec[cur], tout, bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, rows / R, Pm};
-            int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, train, s, pl); });
+            ProfScope ps(0, st);
+            cf* tout = (keep_t && it < d.maxit) ? ht(it + 1) : cspec[1 - cur];
+            PassAArgs pa{cspec[cur], tout, cb, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, crows / R, ppm};
+            int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, train, st, pl); });
             if (e) return e;
         }
         cur = 1 - cur;
         uin = 1 - uin;
     }
+    return 0;
+    };
+    const bool indep = !d.iso && !train && G == 1;  // planes independent of each other
+    // two plane halves on two streams (the caller's and a per-thread auxiliary one), so one half's
+    // pass A runs beside the other half's pass B (ADMM_STREAMS)
+    if (indep && P >= 2 && env_int("ADMM_STREAMS", 1) >= 2) {
+        hipStream_t s2 = aux_stream();
+        if (!s2) return fail(ADMM_TV_EHIP, "auxiliary stream");
+        hipEvent_t fork, join;
+        HIPCHK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(fork, s));
+        HIPCHK(hipStreamWaitEvent(s2, fork, 0));
+        const long long h = P / 2;
+        int e = solve_planes(0, h, h, s);
+        if (!e) e = solve_planes(h, P - h, P - h, s2);
+        HIPCHK(hipEventRecord(join, s2));
+        HIPCHK(hipStreamWaitEvent(s, join, 0));
+        HIPCHK(hipEventDestroy(fork));
+        HIPCHK(hipEventDestroy(join));
+        return e;
+    }
+    const long long chunk = indep ? chunk_planes(H, W, P) : P;
+    for (long long p0 = 0; p0 < P; p0 += chunk)
+        if (int e = solve_planes(p0, std::min(chunk, P - p0), chunk < P ? std::min(chunk, P - p0) : Pm, s)) return e;
     return 0;
 }
 
