@@ -54,6 +54,17 @@ __device__ __forceinline__ cf twid(const cf* __restrict__ tw, int idx) {
     return DIR < 0 ? w : cconj(w);
 }
 
+// x / d for 0 <= x < 2^20, 0 < d, with rd ~ 1/d (v_rcp_f32): the float quotient is within 1 of
+// the true one and one remainder test corrects it -- the transforms' index arithmetic divides by
+// runtime radix products, and the compiler's exact integer division is ~20 instructions
+__device__ __forceinline__ int fdiv(int x, int d, float rd) {
+    int q = (int)((float)x * rd);
+    const int r = x - q * d;
+    q += (r < 0) ? -1 : (r >= d ? 1 : 0);
+    return q;
+}
+__device__ __forceinline__ float frcp(int d) { return __builtin_amdgcn_rcpf((float)d); }
+
 template <int DIR, int R>
 __device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw, int n) {
     if constexpr (R == 2) {
@@ -94,9 +105,11 @@ __device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restr
                                          const cf* __restrict__ tw) {
     const int nb = n / R;                 // butterflies per line
     const int tstride = n / (NS * R);     // twiddle index stride of W_{NS R}
+    const int lg = __ffs(lines) - 1;      // lines is a power of two
+    const float rns = frcp(NS);
     for (int item = threadIdx.x; item < nb * lines; item += blockDim.x) {
-        const int c = item % lines, vt = item / lines;
-        const int m = vt % NS;
+        const int c = item & (lines - 1), vt = item >> lg;
+        const int vq = fdiv(vt, NS, rns), m = vt - vq * NS;
         cf v[R];
 #pragma unroll
         for (int q = 0; q < R; ++q) {
@@ -105,7 +118,7 @@ __device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restr
             v[q] = x;
         }
         small_dft<DIR, R>(v, tw, n);
-        const int base = (vt / NS) * NS * R + m;
+        const int base = vq * NS * R + m;
 #pragma unroll
         for (int k = 0; k < R; ++k) dst[(base + k * NS) * lines + c] = v[k];
     }
@@ -114,10 +127,10 @@ __device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restr
 // any (odd prime) radix R, in two steps:
 //  1. the stage twiddles W_{NS R}^{m q} are applied to the inputs in place (src is this stage's
 //     scratch), so what remains per butterfly is a plain R-point DFT;
-//  2. outputs k and R - k take conjugate twiddles W_R^{+-qk}: an item computes GP such output
-//     pairs of one butterfly (group 0 also output 0), reading each input once and each table
-//     twiddle once for both outputs of a pair -- (1 + GP) LDS reads per input for 2 GP outputs
-//     instead of 2 per input per output, and the two complex products are eight FMAs.
+//  2. outputs k and R - k take conjugate twiddles W_R^{+-qk}, and so do inputs q and R - q: an
+//     item computes GP such output pairs of one butterfly (group 0 also output 0) from the input
+//     sums and differences x_q +- x_{R-q} (real cosine / sine sums), reading each input once and
+//     each table twiddle once per input pair -- four FMAs per input pair and output pair.
 #ifndef ADMM_GP
 #define ADMM_GP 2
 #endif
@@ -132,14 +145,16 @@ __device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict_
     const int nb = n / R;
     const int span = NS * R;
     const int tstride = n / span;
+    const int lg = __ffs(lines) - 1;
+    const float rns = frcp(NS), rnb = frcp(nb);
     if (NS > 1) {
         for (int item = threadIdx.x; item < n * lines; item += blockDim.x) {
-            const int c = item % lines, o = item / lines;  // o = vt + q nb
-            const int vt = o % nb, q = o / nb;
-            const int m = vt % NS;
+            const int c = item & (lines - 1), o = item >> lg;  // o = vt + q nb
+            const int q = fdiv(o, nb, rnb), vt = o - q * nb;
+            const int m = vt - fdiv(vt, NS, rns) * NS;
             if (q > 0 && m > 0) {
                 cf* x = src + (size_t)o * lines + c;
-                *x = cmul(*x, twid<DIR>(tw, ((m * q) % span) * tstride));
+                *x = cmul(*x, twid<DIR>(tw, m * q * tstride));  // m q < NS R: no reduction
             }
         }
         __syncthreads();
@@ -148,48 +163,53 @@ __device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict_
     const int ngrp = (npair + GP - 1) / GP;
     const int rstep = n / R;  // W_R^j = tw[j n / R]
     for (int item = threadIdx.x; item < nb * ngrp * lines; item += blockDim.x) {
-        const int c = item % lines, o = item / lines;
-        const int vt = o % nb, g = o / nb;
-        const int m = vt % NS;
+        const int c = item & (lines - 1), o = item >> lg;
+        const int g = fdiv(o, nb, rnb), vt = o - g * nb;
+        const int vq = fdiv(vt, NS, rns), m = vt - vq * NS;
         const int k0 = 1 + g * GP;
         const cf* col = src + (size_t)vt * lines + c;
         const size_t qstep = (size_t)nb * lines;
         cf x0 = col[0];
         cf acc0 = x0;  // output 0 (group 0 only)
-        cf ap[GP], am[GP];
+        // inputs q and R - q share the twiddle pair w, conj(w) (w = W_R^{qk}):
+        //   x_q w + x_{R-q} conj(w) = s w.x + i d w.y,   x_q conj(w) + x_{R-q} w = s w.x - i d w.y
+        // with s = x_q + x_{R-q}, d = x_q - x_{R-q}: four FMAs per input pair for both outputs
+        // k and R - k (the real cosine / sine sums), half the loop trips of the per-input form
+        cf sa[GP], sb[GP];  // sum s w.x, sum d w.y
         int idx[GP];  // table index (q (k0 + j) mod R) * rstep, stepped without multiply or modulo
         const int wrap = R * rstep;
 #pragma unroll
         for (int j = 0; j < GP; ++j) {
-            ap[j] = x0;
-            am[j] = x0;
+            sa[j] = mkc(0.f, 0.f);
+            sb[j] = mkc(0.f, 0.f);
             idx[j] = 0;
         }
 #pragma unroll ADMM_GUNROLL
-        for (int q = 1; q < R; ++q) {
-            const cf x = col[q * qstep];
-            acc0 = cadd(acc0, x);
+        for (int q = 1; q <= npair; ++q) {
+            const cf xa = col[q * qstep], xb = col[(R - q) * qstep];
+            const cf s = cadd(xa, xb), d = csub(xa, xb);
+            acc0 = cadd(acc0, s);
 #pragma unroll
             for (int j = 0; j < GP; ++j) {
                 idx[j] += (k0 + j) * rstep;
                 if (idx[j] >= wrap) idx[j] -= wrap;
                 const cf w = twid<DIR>(tw, idx[j]);
-                // x w and x conj(w) accumulated with eight FMAs
-                ap[j].x = fmaf(-x.y, w.y, fmaf(x.x, w.x, ap[j].x));
-                ap[j].y = fmaf(x.y, w.x, fmaf(x.x, w.y, ap[j].y));
-                am[j].x = fmaf(x.y, w.y, fmaf(x.x, w.x, am[j].x));
-                am[j].y = fmaf(-x.x, w.y, fmaf(x.y, w.x, am[j].y));
+                sa[j].x = fmaf(s.x, w.x, sa[j].x);
+                sa[j].y = fmaf(s.y, w.x, sa[j].y);
+                sb[j].x = fmaf(d.x, w.y, sb[j].x);
+                sb[j].y = fmaf(d.y, w.y, sb[j].y);
             }
         }
-        cf* out = dst + ((size_t)(vt / NS) * span + m) * lines + c;
+        cf* out = dst + ((size_t)vq * span + m) * lines + c;
         const size_t kstep = (size_t)NS * lines;
         if (g == 0) out[0] = acc0;
 #pragma unroll
         for (int j = 0; j < GP; ++j) {
             const int k = k0 + j;
             if (k <= npair) {
-                out[k * kstep] = ap[j];
-                out[(R - k) * kstep] = am[j];
+                const cf a = cadd(x0, sa[j]);
+                out[k * kstep] = mkc(a.x - sb[j].y, a.y + sb[j].x);        // a + i sb
+                out[(R - k) * kstep] = mkc(a.x + sb[j].y, a.y - sb[j].x);  // a - i sb
             }
         }
     }
@@ -216,11 +236,13 @@ __device__ __forceinline__ void gstage_blue(const cf* __restrict__ src, cf* __re
     const int nb = n / R, span = NS * R, tstride = n / span;
     const int items = nb * lines;
     const int rounds = (items + nsg - 1) / nsg;
+    const int lg = __ffs(lines) - 1;
+    const float rns = frcp(NS);
     for (int rr = 0; rr < rounds; ++rr) {
         const int item = rr * nsg + sg;
         const bool live = item < items;
-        const int c = live ? item % lines : 0, vt = live ? item / lines : 0;
-        const int m = vt % NS;
+        const int c = live ? item & (lines - 1) : 0, vt = live ? item >> lg : 0;
+        const int vq = fdiv(vt, NS, rns), m = vt - vq * NS;
         cf v[E];
 #pragma unroll
         for (int j = 0; j < E; ++j) {
@@ -228,7 +250,7 @@ __device__ __forceinline__ void gstage_blue(const cf* __restrict__ src, cf* __re
             cf x = mkc(0.f, 0.f);
             if (live && q < R) {
                 x = src[(vt + q * nb) * lines + c];
-                if (q > 0 && m > 0) x = cmul(x, twid<DIR>(tw, ((m * q) % span) * tstride));
+                if (q > 0 && m > 0) x = cmul(x, twid<DIR>(tw, m * q * tstride));
                 x = DIR < 0 ? cmul(x, chirp[q]) : cmulc(x, chirp[q]);
             }
             v[j] = x;
@@ -237,7 +259,7 @@ __device__ __forceinline__ void gstage_blue(const cf* __restrict__ src, cf* __re
 #pragma unroll
         for (int j = 0; j < E; ++j) v[j] = DIR < 0 ? cmul(v[j], Bf[t + L * j]) : cmulc(v[j], Bf[t + L * j]);
         fft<M, L, +1, 0, 1>(v, buf, twM, t);
-        cf* out = dst + ((size_t)(vt / NS) * span + m) * lines + c;
+        cf* out = dst + ((size_t)vq * span + m) * lines + c;
 #pragma unroll
         for (int j = 0; j < E; ++j) {
             const int k = t + L * j;
@@ -348,22 +370,22 @@ __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
     const cf* tw = TWG ? a.tw : twl;
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);  // real rows in this block
-    for (int idx = threadIdx.x; idx < W * 2 * lines; idx += blockDim.x) {
-        const int rr = idx / W, i = idx % W;  // coalesced along the row
-        const float v = rr < nl ? a.img[(r0 + rr) * W + i] : 0.f;
-        float* slot = reinterpret_cast<float*>(&A[i * lines + (rr >> 1)]);
-        slot[rr & 1] = v;  // even row -> real part, odd row -> imaginary part
-    }
+    for (int rr = 0; rr < 2 * lines; ++rr)  // coalesced along the row
+        for (int i = threadIdx.x; i < W; i += blockDim.x) {
+            const float v = rr < nl ? a.img[(r0 + rr) * W + i] : 0.f;
+            float* slot = reinterpret_cast<float*>(&A[i * lines + (rr >> 1)]);
+            slot[rr & 1] = v;  // even row -> real part, odd row -> imaginary part
+        }
     __syncthreads();
     const cf* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
-    for (int idx = threadIdx.x; idx < Wh * lines; idx += blockDim.x) {
-        const int c = idx / Wh, k = idx % Wh;
-        const cf z = res[k * lines + c];
-        const cf m = res[((W - k) % W) * lines + c];
-        const long long ra = r0 + 2 * c;
-        if (2 * c < nl) a.spec[ra * Wh + k] = mkc(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));
-        if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkc(0.5f * (z.y + m.y), 0.5f * (m.x - z.x));
-    }
+    for (int c = 0; c < lines; ++c)
+        for (int k = threadIdx.x; k < Wh; k += blockDim.x) {
+            const cf z = res[k * lines + c];
+            const cf m = res[(k == 0 ? 0 : W - k) * lines + c];
+            const long long ra = r0 + 2 * c;
+            if (2 * c < nl) a.spec[ra * Wh + k] = mkc(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));
+            if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkc(0.5f * (z.y + m.y), 0.5f * (m.x - z.x));
+        }
 }
 
 template <int BM, bool TWG>
@@ -389,22 +411,20 @@ __global__ void __launch_bounds__(256) k_grow_inv(GRowArgs a) {
         }
         return cconj(a.spec[row * Wh + (W - k)]);
     };
-    for (int idx = threadIdx.x; idx < W * lines; idx += blockDim.x) {
-        const int c = idx / W, k = idx % W;
-        const long long ra = r0 + 2 * c;
-        const cf xa = 2 * c < nl ? full(ra, k) : mkc(0.f, 0.f);
-        const cf xb = 2 * c + 1 < nl ? full(ra + 1, k) : mkc(0.f, 0.f);
-        A[k * lines + c] = mkc(xa.x - xb.y, xa.y + xb.x);  // Z = Xa + i Xb
-    }
+    for (int c = 0; c < lines; ++c)
+        for (int k = threadIdx.x; k < W; k += blockDim.x) {
+            const long long ra = r0 + 2 * c;
+            const cf xa = 2 * c < nl ? full(ra, k) : mkc(0.f, 0.f);
+            const cf xb = 2 * c + 1 < nl ? full(ra + 1, k) : mkc(0.f, 0.f);
+            A[k * lines + c] = mkc(xa.x - xb.y, xa.y + xb.x);  // Z = Xa + i Xb
+        }
     __syncthreads();
     const cf* res = gfft_lds<+1, BM>(A, B, a.plan, lines, tw, X);
-    for (int idx = threadIdx.x; idx < W * 2 * lines; idx += blockDim.x) {
-        const int rr = idx / W, i = idx % W;
-        if (rr < nl) {
+    for (int rr = 0; rr < nl; ++rr)
+        for (int i = threadIdx.x; i < W; i += blockDim.x) {
             const cf z = res[i * lines + (rr >> 1)];
             a.img_out[(r0 + rr) * W + i] = (rr & 1) ? z.y : z.x;
         }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -430,6 +450,7 @@ template <int MODE, int BM, bool TWG>
 __global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
+    const int lgc = __ffs(cols) - 1;  // cols is a power of two
     cf* twl = reinterpret_cast<cf*>(smem);
     cf* A = twl + (TWG ? 0 : H + a.plan.ntab);
     cf* B = A + (size_t)H * cols;
@@ -442,7 +463,7 @@ __global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
     const int nc = min(cols, Wh - c0);
     cf* S = a.spec + (size_t)p * H * Wh + c0;
     for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
-        const int i = idx / cols, c = idx % cols;  // coalesced across the block's columns
+        const int i = idx >> lgc, c = idx & (cols - 1);  // coalesced across the block's columns
         A[i * cols + c] = c < nc ? S[(size_t)i * Wh + c] : mkc(0.f, 0.f);
     }
     __syncthreads();
@@ -451,13 +472,13 @@ __global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
     if (a.dump) {
         cf* D = a.dump + (size_t)p * H * Wh + c0;
         for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
-            const int i = idx / cols, c = idx % cols;
+            const int i = idx >> lgc, c = idx & (cols - 1);
             if (c < nc) D[(size_t)i * Wh + c] = res[i * cols + c];
         }
     }
     if constexpr (MODE == 3) return;
     for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
-        const int ky = idx / cols, c = idx % cols;
+        const int ky = idx >> lgc, c = idx & (cols - 1);
         if (c >= nc) continue;
         const size_t f = (size_t)(c0 + c) * H + ky;
         cf v = res[ky * cols + c];
@@ -469,7 +490,7 @@ __global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
     __syncthreads();
     const cf* out = gfft_lds<+1, BM>(res, other, a.plan, cols, tw, X);
     for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
-        const int i = idx / cols, c = idx % cols;
+        const int i = idx >> lgc, c = idx & (cols - 1);
         if (c < nc) S[(size_t)i * Wh + c] = out[i * cols + c];
     }
 }
