@@ -755,7 +755,11 @@ int gapply(const float* img_in, float* img_out, cf* spec, const Layout& Lo, void
 }
 
 int gstep(const GStepArgs& a, bool iso, bool first, bool hist, hipStream_t s) {
-    const dim3 grid((unsigned)((a.npx + 255) / 256)), blk(256);
+    // one block row per image row (P H <= 2^31 - 1 rows), column chunks of 256 pixels
+    const long long rows = a.npx / a.W;
+    if (rows <= 0) return 0;
+    if (rows > 0x7fffffffLL) return fail(ADMM_TV_EUNSUPPORTED, "too many image rows for the generic step kernel");
+    const dim3 grid((unsigned)rows, (unsigned)((a.W + 255) / 256)), blk(256);
     const int sel = (iso ? 4 : 0) | (first ? 2 : 0) | (hist ? 1 : 0);
     switch (sel) {
         case 0: hipLaunchKernelGGL((k_gstep<false, false, false>), grid, blk, 0, s, a); break;

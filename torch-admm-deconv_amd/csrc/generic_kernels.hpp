@@ -65,6 +65,27 @@ __device__ __forceinline__ int fdiv(int x, int d, float rd) {
 }
 __device__ __forceinline__ float frcp(int d) { return __builtin_amdgcn_rcpf((float)d); }
 
+// cos / sin(2 pi m / R), m in [0, R), for the odd radices 3, 5, 7 (fp64 literals rounded to fp32)
+template <int R> struct OddTw;
+template <> struct OddTw<3> {
+    static constexpr double C[2] = {1.0, -0.5};
+    static constexpr double S[2] = {0.0, 0.86602540378443864676};
+    static constexpr float cosv(int m) { return (float)C[m <= 1 ? m : 3 - m]; }
+    static constexpr float sinv(int m) { return (float)(m <= 1 ? S[m] : -S[3 - m]); }
+};
+template <> struct OddTw<5> {
+    static constexpr double C[3] = {1.0, 0.30901699437494742410, -0.80901699437494742410};
+    static constexpr double S[3] = {0.0, 0.95105651629515357212, 0.58778525229247312917};
+    static constexpr float cosv(int m) { return (float)C[m <= 2 ? m : 5 - m]; }
+    static constexpr float sinv(int m) { return (float)(m <= 2 ? S[m] : -S[5 - m]); }
+};
+template <> struct OddTw<7> {
+    static constexpr double C[4] = {1.0, 0.62348980185873353053, -0.22252093395631440429, -0.90096886790241912624};
+    static constexpr double S[4] = {0.0, 0.78183148246802980871, 0.97492791218182360702, 0.43388373911755812048};
+    static constexpr float cosv(int m) { return (float)C[m <= 3 ? m : 7 - m]; }
+    static constexpr float sinv(int m) { return (float)(m <= 3 ? S[m] : -S[7 - m]); }
+};
+
 template <int DIR, int R>
 __device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw, int n) {
     if constexpr (R == 2) {
@@ -80,6 +101,40 @@ __device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw,
         v[3] = csub(t1, t3);
     } else if constexpr (R == 8 || R == 16) {
         DFT<R, DIR>::template run<1, 0>(v);  // register DFT with exact constant twiddles (fft_core.hpp)
+    } else if constexpr (R == 3 || R == 5 || R == 7) {
+        // odd R with compile-time cosines / sines on the input sums / differences (the pairing of
+        // gstage_any): y_k, y_{R-k} = x0 + sum_q s_q cos(qk) -+ DIR i sum_q d_q sin(qk)
+        constexpr int h = (R - 1) / 2;
+        cf s[h + 1], d[h + 1];
+        cf y0 = v[0];
+        static_for<1, h + 1>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            s[q] = cadd(v[q], v[R - q]);
+            d[q] = csub(v[q], v[R - q]);
+            y0 = cadd(y0, s[q]);
+        });
+        cf out[R];
+        out[0] = y0;
+        static_for<1, h + 1>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            cf a = v[0], b = mkc(0.f, 0.f);
+            static_for<1, h + 1>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                constexpr float c = OddTw<R>::cosv((q * k) % R), sn = OddTw<R>::sinv((q * k) % R);
+                a.x = fmaf(s[q].x, c, a.x);
+                a.y = fmaf(s[q].y, c, a.y);
+                b.x = fmaf(d[q].x, sn, b.x);
+                b.y = fmaf(d[q].y, sn, b.y);
+            });
+            // i b = (-b.y, b.x); forward (DIR < 0): y_k = a - i b
+            const cf ib = mkc(-b.y, b.x);
+            out[k] = DIR < 0 ? csub(a, ib) : cadd(a, ib);
+            out[R - k] = DIR < 0 ? cadd(a, ib) : csub(a, ib);
+        });
+#pragma unroll
+        for (int k = 0; k < R; ++k) v[k] = out[k];
+        (void)tw;
+        (void)n;
     } else {
         // y_k = sum_q v_q W_R^{qk}, W_R^j = tw[j n / R]
         cf y[R];
@@ -530,12 +585,16 @@ __device__ __forceinline__ float gprev_u(const float* __restrict__ src, const fl
 
 template <bool ISO, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256) k_gstep(GStepArgs a) {
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.npx) return;
+    // grid (rows P H, column chunks): one 32-bit division per thread instead of 64-bit ones
     const int H = a.H, W = a.W;
+    const int j = (int)(blockIdx.y * blockDim.x + threadIdx.x);
+    if (j >= W) return;
+    const unsigned row = blockIdx.x;
+    const int i = (int)(row % (unsigned)H);
+    const long long pb = (long long)(row - (unsigned)i) * W;
+    const long long idx = pb + (long long)i * W + j;
+    const int rem = i * W + j;
     const long long HW = (long long)H * W;
-    const long long pb = idx - idx % HW;
-    const int rem = (int)(idx % HW), i = rem / W, j = rem % W;
     const int jm = j == 0 ? W - 1 : j - 1, jp = j == W - 1 ? 0 : j + 1;
     const int im = i == 0 ? H - 1 : i - 1, ip = i == H - 1 ? 0 : i + 1;
     const size_t P0 = (size_t)idx, PR = (size_t)(pb + (long long)i * W + jp), PD = (size_t)(pb + (long long)ip * W + j);
