@@ -100,6 +100,20 @@ def test_bluestein_matches_direct_prime_stages(cuda_dev, shape, monkeypatch):
     assert e_blue <= 2 * e_direct + 1e-6
 
 
+@pytest.mark.parametrize("shape,iso", [((2, 3, 321, 481), False), ((1, 3, 100, 75), True), ((2, 1, 7, 9), False)])
+def test_fused_step_is_bit_identical(cuda_dev, shape, iso, monkeypatch):
+    """The inference path runs the per-pixel step inside the row transform of r
+    (k_grow_fwd_step); the separate kernels (ADMM_GSTEP_FUSE=0) give the same bits."""
+    from admmtor.synth import blurred_batch, make_psf
+    k = make_psf("gauss:1.5", 5)
+    x = blurred_batch(*shape, k, seed=3)
+    monkeypatch.setenv("ADMM_GSTEP_FUSE", "0")
+    a = solve(x, k, 0.01, 0.02, iso, 12, cuda_dev)
+    monkeypatch.setenv("ADMM_GSTEP_FUSE", "1")
+    b = solve(x, k, 0.01, 0.02, iso, 12, cuda_dev)
+    assert torch.equal(a, b)
+
+
 def test_generic_psf_transpose(cuda_dev):
     import ctypes
     from admmtor import _native

@@ -705,6 +705,28 @@ int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hi
         return launch_check("k_grow_fwd");
     });
 }
+// the step fused into the row transform of r (k_grow_fwd_step; inference iterations)
+template <bool ISO, bool FIRST>
+int grow_fwd_step_t(const GStepArgs& g, cf* spec, const cf* tw, int W, long long rows, hipStream_t s) {
+    const GPlan pl = make_plan(W);
+    GRowArgs a{nullptr, spec, nullptr, tw, pl, rows, grow_lines(W, pl)};
+    const size_t lds = glds(W, a.lines, a.plan);
+    return with_plan(a.plan, [&](auto bm, auto twg) {
+        constexpr int BM = decltype(bm)::value;
+        constexpr bool TWG = decltype(twg)::value;
+        if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))),
+                           dim3(gen_threads("ADMM_GROW_NT")), lds, s, a, g);
+        return launch_check("k_grow_fwd_step");
+    });
+}
+int grow_fwd_step(const GStepArgs& g, cf* spec, const cf* tw, int W, long long rows, bool iso, bool first,
+                  hipStream_t s) {
+    if (iso) return first ? grow_fwd_step_t<true, true>(g, spec, tw, W, rows, s)
+                          : grow_fwd_step_t<true, false>(g, spec, tw, W, rows, s);
+    return first ? grow_fwd_step_t<false, true>(g, spec, tw, W, rows, s)
+                 : grow_fwd_step_t<false, false>(g, spec, tw, W, rows, s);
+}
 int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hipStream_t s) {
     const GPlan pl = make_plan(W);
     GRowArgs a{nullptr, const_cast<cf*>(spec), img, tw, pl, rows, grow_lines(W, pl)};
@@ -896,9 +918,14 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, c
         {
             ProfScope ps(0, s);
             GStepArgs ga{xk, bimg, uxi, uyi, uxo, uyo, last ? nullptr : rimg, nsq, nprev, lam, rho, H, W, npx};
-            if (int e = gstep(ga, d.iso != 0, first, train, s)) return e;
-            if (!last)
-                if (int e = grow_fwd(rimg, spec, twW, W, rows, s)) return e;
+            // inference: the step runs inside the row transform of r (ADMM_GSTEP_FUSE=0: separate)
+            if (!train && !last && env_int("ADMM_GSTEP_FUSE", 1)) {
+                if (int e = grow_fwd_step(ga, spec, twW, W, rows, d.iso != 0, first, s)) return e;
+            } else {
+                if (int e = gstep(ga, d.iso != 0, first, train, s)) return e;
+                if (!last)
+                    if (int e = grow_fwd(rimg, spec, twW, W, rows, s)) return e;
+            }
         }
         uin = 1 - uin;
     }

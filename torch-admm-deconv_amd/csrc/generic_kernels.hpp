@@ -583,13 +583,11 @@ __device__ __forceinline__ float gprev_u(const float* __restrict__ src, const fl
     }
 }
 
+// one pixel (image row `row` of P H, column j) of the step: writes u_k and returns r_{k+1}
+// (b + rho D^T w; unused when a.r is null in k_gstep)
 template <bool ISO, bool FIRST, bool HIST>
-__global__ void __launch_bounds__(256) k_gstep(GStepArgs a) {
-    // grid (rows P H, column chunks): one 32-bit division per thread instead of 64-bit ones
+__device__ __forceinline__ float gstep_px(const GStepArgs& a, unsigned row, int j) {
     const int H = a.H, W = a.W;
-    const int j = (int)(blockIdx.y * blockDim.x + threadIdx.x);
-    if (j >= W) return;
-    const unsigned row = blockIdx.x;
     const int i = (int)(row % (unsigned)H);
     const long long pb = (long long)(row - (unsigned)i) * W;
     const long long idx = pb + (long long)i * W + j;
@@ -628,10 +626,51 @@ __global__ void __launch_bounds__(256) k_gstep(GStepArgs a) {
     const float wxR = zxR - (axR - zxR), wyD = zyD - (ayD - zyD);
     a.uxo[P0] = HIST ? ax : nux;
     a.uyo[P0] = HIST ? ay : nuy;
-    if (a.r) {
-        const float v = (wx - wxR) + (wy - wyD);
-        a.r[P0] = fmaf(rho, v, a.b[P0]);
-    }
+    const float v = (wx - wxR) + (wy - wyD);
+    return fmaf(rho, v, a.b[P0]);
+}
+
+template <bool ISO, bool FIRST, bool HIST>
+__global__ void __launch_bounds__(256) k_gstep(GStepArgs a) {
+    // grid (rows P H, column chunks): one 32-bit division per thread instead of 64-bit ones
+    const int j = (int)(blockIdx.y * blockDim.x + threadIdx.x);
+    if (j >= a.W) return;
+    const float r = gstep_px<ISO, FIRST, HIST>(a, blockIdx.x, j);
+    if (a.r) a.r[(size_t)blockIdx.x * a.W + j] = r;
+}
+
+// the step fused into the next row transform (inference): a block computes r_{k+1} for its
+// 2 lines rows pixel by pixel (gstep_px, writing u_k) straight into the LDS image of k_grow_fwd,
+// so r never goes through HBM (-8 B/px and one launch per iteration)
+template <int BM, bool TWG, bool ISO, bool FIRST>
+__global__ void __launch_bounds__(256) k_grow_fwd_step(GRowArgs a, GStepArgs g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
+    cf* twl = reinterpret_cast<cf*>(smem);
+    cf* A = twl + (TWG ? 0 : W + a.plan.ntab);
+    cf* B = A + (size_t)W * lines;
+    cf* X = B + (size_t)W * lines;
+    if constexpr (!TWG)
+        for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
+    const cf* tw = TWG ? a.tw : twl;
+    const long long r0 = (long long)blockIdx.x * 2 * lines;
+    const int nl = (int)min((long long)2 * lines, a.rows - r0);
+    for (int rr = 0; rr < 2 * lines; ++rr)
+        for (int i = threadIdx.x; i < W; i += blockDim.x) {
+            const float v = rr < nl ? gstep_px<ISO, FIRST, false>(g, (unsigned)(r0 + rr), i) : 0.f;
+            float* slot = reinterpret_cast<float*>(&A[i * lines + (rr >> 1)]);
+            slot[rr & 1] = v;
+        }
+    __syncthreads();
+    const cf* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
+    for (int c = 0; c < lines; ++c)
+        for (int k = threadIdx.x; k < Wh; k += blockDim.x) {
+            const cf z = res[k * lines + c];
+            const cf m = res[(k == 0 ? 0 : W - k) * lines + c];
+            const long long ra = r0 + 2 * c;
+            if (2 * c < nl) a.spec[ra * Wh + k] = mkc(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));
+            if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkc(0.5f * (z.y + m.y), 0.5f * (m.x - z.x));
+        }
 }
 
 // iso: N_k[pixel] = sum over planes of a_x^2, a_y^2 with a = D x_k + u_{k-1}
