@@ -563,7 +563,7 @@ GPlan make_plan(int n) {
     int M = 0;  // one Bluestein size for the plan: M = 2^k >= 2R - 1 for its largest such prime
     for (int s = 0; s < p.nst; ++s) {
         const int R = p.rad[s];
-        if (bmin <= 0 || R <= 7 || R < bmin || 2 * R - 1 > 1024) continue;
+        if (bmin <= 0 || R <= 7 || (R & (R - 1)) == 0 || R < bmin || 2 * R - 1 > 1024) continue;  // primes only
         int m = 32;
         while (m < 2 * R - 1) m *= 2;
         M = std::max(M, m);
@@ -571,7 +571,7 @@ GPlan make_plan(int n) {
     int off = n;
     for (int s = 0; s < p.nst; ++s) {
         const int R = p.rad[s];
-        const bool blue = M > 0 && R > 7 && R >= bmin && 2 * R - 1 <= 1024;
+        const bool blue = M > 0 && R > 7 && (R & (R - 1)) != 0 && R >= bmin && 2 * R - 1 <= 1024;
         p.bst[s] = blue ? M : 0;
         p.boff[s] = blue ? off : 0;
         if (blue) off += R + 2 * M;
