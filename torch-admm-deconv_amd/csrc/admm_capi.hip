@@ -578,7 +578,7 @@ GPlan make_plan(int n) {
     }
     p.bm = M;
     p.ntab = off - n;
-    p.xslots = M > 0 ? (256 / (M / blue_e(M))) * (M + M / 8) : 0;
+    p.xslots = M > 0 ? (GNT / (M / blue_e(M))) * (M + M / 8) : 0;
     // one line must fit the LDS: else no Bluestein, else twiddles from global memory
     if (glds(n, 1, p) <= kMaxLds) return p;
     GPlan q = make_plan_radices(n);
@@ -590,8 +590,8 @@ bool gen_fits(int n) { return glds(n, 1, make_plan(n)) <= kMaxLds; }
 
 // threads per block of the generic transform kernels (A/B knob; 64, 128 or 256)
 int gen_threads(const char* knob) {
-    const int v = env_int(knob, 256);
-    return v <= 64 ? 64 : v <= 128 ? 128 : 256;
+    const int v = env_int(knob, GNT);
+    return v <= 64 ? 64 : v <= 128 ? 128 : v <= 256 || GNT <= 256 ? 256 : GNT;
 }
 
 template <class F> int with_plan(const GPlan& p, F&& f) {
@@ -686,7 +686,7 @@ int gcol_cols(int H, const GPlan& p) {
         int nb = H;  // butterflies per line of the Bluestein stages (fewest)
         for (int s = 0; s < p.nst; ++s)
             if (p.bst[s] > 0) nb = std::min(nb, H / p.rad[s]);
-        const int nsg = 256 / (p.bm / blue_e(p.bm));
+        const int nsg = GNT / (p.bm / blue_e(p.bm));
         while (dflt * nb < nsg && dflt < 16) dflt *= 2;
     }
     return fit_lines(H, pow2_floor(std::max(1, std::min(32, env_int("ADMM_GCOL_COLS", dflt)))), p);

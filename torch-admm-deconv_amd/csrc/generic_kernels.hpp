@@ -21,7 +21,12 @@
 
 namespace admm {
 
-constexpr int GMAXST = 24;  // max number of radix stages (n <= 8192 -> at most 13 factors)
+constexpr int GMAXST = 24;
+// threads per block of the generic transform kernels (-DADMM_GNT=512 for A/B runs)
+#ifndef ADMM_GNT
+#define ADMM_GNT 256
+#endif
+constexpr int GNT = ADMM_GNT;  // max number of radix stages (n <= 8192 -> at most 13 factors)
 
 // A stage whose radix is a prime R > 7 runs either as the O(R)-per-output stage (gstage_any) or,
 // for R >= the Bluestein threshold (admm_capi.hip make_plan), as a chirp-z transform: the R-point
@@ -413,7 +418,7 @@ struct GRowArgs {
 // TWG: twiddles / tables read from global memory (GPlan::twg; a template parameter, so the LDS
 // variant keeps its LDS reads)
 template <int BM, bool TWG>
-__global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
+__global__ void __launch_bounds__(GNT) k_grow_fwd(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     cf* twl = reinterpret_cast<cf*>(smem);
@@ -444,7 +449,7 @@ __global__ void __launch_bounds__(256) k_grow_fwd(GRowArgs a) {
 }
 
 template <int BM, bool TWG>
-__global__ void __launch_bounds__(256) k_grow_inv(GRowArgs a) {
+__global__ void __launch_bounds__(GNT) k_grow_inv(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     cf* twl = reinterpret_cast<cf*>(smem);
@@ -502,7 +507,7 @@ struct GColArgs {
 };
 
 template <int MODE, int BM, bool TWG>
-__global__ void __launch_bounds__(256) k_gcol(GColArgs a) {
+__global__ void __launch_bounds__(GNT) k_gcol(GColArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
     const int lgc = __ffs(cols) - 1;  // cols is a power of two
@@ -643,7 +648,7 @@ __global__ void __launch_bounds__(256) k_gstep(GStepArgs a) {
 // 2 lines rows pixel by pixel (gstep_px, writing u_k) straight into the LDS image of k_grow_fwd,
 // so r never goes through HBM (-8 B/px and one launch per iteration)
 template <int BM, bool TWG, bool ISO, bool FIRST>
-__global__ void __launch_bounds__(256) k_grow_fwd_step(GRowArgs a, GStepArgs g) {
+__global__ void __launch_bounds__(GNT) k_grow_fwd_step(GRowArgs a, GStepArgs g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     cf* twl = reinterpret_cast<cf*>(smem);
