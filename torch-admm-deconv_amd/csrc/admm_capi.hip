@@ -594,6 +594,16 @@ int gen_threads(const char* knob) {
     return v <= 64 ? 64 : v <= 128 ? 128 : v <= 256 || GNT <= 256 ? 256 : GNT;
 }
 
+// long lines without Bluestein stages run their transform blocks with 512 threads (a 1,920-point
+// row's stages have 480-960 butterflies; 256 threads leave them latency-bound: HD 1080x1920
+// 716 -> 850 it/s; BSD-like lines with Bluestein stages are faster at 256).  ADMM_GEN_WIDE_MIN:
+// the line length from which it applies (0: never).
+constexpr int kGenWide = 512;
+bool gen_wide(int n, const GPlan& p) {
+    const int mn = env_int("ADMM_GEN_WIDE_MIN", 1024);
+    return p.bm == 0 && mn > 0 && n >= mn;
+}
+
 template <class F> int with_plan(const GPlan& p, F&& f) {
     if (p.twg) return f(std::integral_constant<int, 0>{}, std::true_type{});
     return with_bm(p.bm, [&](auto bm) { return f(bm, std::false_type{}); });
@@ -699,9 +709,16 @@ int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hi
     return with_plan(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
+        const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
+        if constexpr (BM == 0) {
+            if (gen_wide(W, pl)) {
+                if (int e = set_lds(k_grow_fwd<BM, TWG, kGenWide>, lds)) return e;
+                hipLaunchKernelGGL((k_grow_fwd<BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
+                return launch_check("k_grow_fwd");
+            }
+        }
         if (int e = set_lds(k_grow_fwd<BM, TWG>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_fwd<BM, TWG>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))),
-                           dim3(gen_threads("ADMM_GROW_NT")), lds, s, a);
+        hipLaunchKernelGGL((k_grow_fwd<BM, TWG>), grid, dim3(gen_threads("ADMM_GROW_NT")), lds, s, a);
         return launch_check("k_grow_fwd");
     });
 }
@@ -714,9 +731,16 @@ int grow_fwd_step_t(const GStepArgs& g, cf* spec, const cf* tw, int W, long long
     return with_plan(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
+        const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
+        if constexpr (BM == 0) {
+            if (gen_wide(W, pl)) {
+                if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST, kGenWide>, lds)) return e;
+                hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST, kGenWide>), grid, dim3(kGenWide), lds, s, a, g);
+                return launch_check("k_grow_fwd_step");
+            }
+        }
         if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))),
-                           dim3(gen_threads("ADMM_GROW_NT")), lds, s, a, g);
+        hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST>), grid, dim3(gen_threads("ADMM_GROW_NT")), lds, s, a, g);
         return launch_check("k_grow_fwd_step");
     });
 }
@@ -734,13 +758,27 @@ int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hi
     return with_plan(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
+        const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
+        if constexpr (BM == 0) {
+            if (gen_wide(W, pl)) {
+                if (int e = set_lds(k_grow_inv<BM, TWG, kGenWide>, lds)) return e;
+                hipLaunchKernelGGL((k_grow_inv<BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
+                return launch_check("k_grow_inv");
+            }
+        }
         if (int e = set_lds(k_grow_inv<BM, TWG>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_inv<BM, TWG>), dim3((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines))),
-                           dim3(gen_threads("ADMM_GROW_NT")), lds, s, a);
+        hipLaunchKernelGGL((k_grow_inv<BM, TWG>), grid, dim3(gen_threads("ADMM_GROW_NT")), lds, s, a);
         return launch_check("k_grow_inv");
     });
 }
 template <int MODE, int BM, bool TWG> int gcol_launch(const GColArgs& a, size_t lds, dim3 grid, hipStream_t s) {
+    if constexpr (BM == 0) {
+        if (gen_wide(a.plan.n, a.plan)) {
+            if (int e = set_lds(k_gcol<MODE, BM, TWG, kGenWide>, lds)) return e;
+            hipLaunchKernelGGL((k_gcol<MODE, BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
+            return launch_check("k_gcol");
+        }
+    }
     if (int e = set_lds(k_gcol<MODE, BM, TWG>, lds)) return e;
     hipLaunchKernelGGL((k_gcol<MODE, BM, TWG>), grid, dim3(gen_threads("ADMM_GCOL_NT")), lds, s, a);
     return launch_check("k_gcol");

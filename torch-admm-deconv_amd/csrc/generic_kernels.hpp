@@ -417,8 +417,8 @@ struct GRowArgs {
 // holds `lines` complex rows = 2 * lines real rows.
 // TWG: twiddles / tables read from global memory (GPlan::twg; a template parameter, so the LDS
 // variant keeps its LDS reads)
-template <int BM, bool TWG>
-__global__ void __launch_bounds__(GNT) k_grow_fwd(GRowArgs a) {
+template <int BM, bool TWG, int NT = GNT>
+__global__ void __launch_bounds__(NT) k_grow_fwd(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     cf* twl = reinterpret_cast<cf*>(smem);
@@ -448,8 +448,8 @@ __global__ void __launch_bounds__(GNT) k_grow_fwd(GRowArgs a) {
         }
 }
 
-template <int BM, bool TWG>
-__global__ void __launch_bounds__(GNT) k_grow_inv(GRowArgs a) {
+template <int BM, bool TWG, int NT = GNT>
+__global__ void __launch_bounds__(NT) k_grow_inv(GRowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     cf* twl = reinterpret_cast<cf*>(smem);
@@ -506,8 +506,8 @@ struct GColArgs {
     long long P;
 };
 
-template <int MODE, int BM, bool TWG>
-__global__ void __launch_bounds__(GNT) k_gcol(GColArgs a) {
+template <int MODE, int BM, bool TWG, int NT = GNT>
+__global__ void __launch_bounds__(NT) k_gcol(GColArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
     const int lgc = __ffs(cols) - 1;  // cols is a power of two
@@ -647,8 +647,8 @@ __global__ void __launch_bounds__(256) k_gstep(GStepArgs a) {
 // the step fused into the next row transform (inference): a block computes r_{k+1} for its
 // 2 lines rows pixel by pixel (gstep_px, writing u_k) straight into the LDS image of k_grow_fwd,
 // so r never goes through HBM (-8 B/px and one launch per iteration)
-template <int BM, bool TWG, bool ISO, bool FIRST>
-__global__ void __launch_bounds__(GNT) k_grow_fwd_step(GRowArgs a, GStepArgs g) {
+template <int BM, bool TWG, bool ISO, bool FIRST, int NT = GNT>
+__global__ void __launch_bounds__(NT) k_grow_fwd_step(GRowArgs a, GStepArgs g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     cf* twl = reinterpret_cast<cf*>(smem);
