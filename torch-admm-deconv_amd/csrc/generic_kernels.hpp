@@ -590,8 +590,12 @@ __device__ __forceinline__ float gprev_u(const float* __restrict__ src, const fl
 
 // one pixel (image row `row` of P H, column j) of the step: writes u_k and returns r_{k+1}
 // (b + rho D^T w; unused when a.r is null in k_gstep)
+// (the image pointers as __restrict__ parameters: after inlining the compiler may move one
+// pixel's loads above another's stores, so a thread's pixels overlap their memory latency)
 template <bool ISO, bool FIRST, bool HIST>
-__device__ __forceinline__ float gstep_px(const GStepArgs& a, unsigned row, int j) {
+__device__ __forceinline__ float gstep_pxr(const GStepArgs& a, const float* __restrict__ xs, const float* __restrict__ bs,
+                                           const float* __restrict__ uxs, const float* __restrict__ uys,
+                                           float* __restrict__ uxd, float* __restrict__ uyd, unsigned row, int j) {
     const int H = a.H, W = a.W;
     const int i = (int)(row % (unsigned)H);
     const long long pb = (long long)(row - (unsigned)i) * W;
@@ -604,15 +608,15 @@ __device__ __forceinline__ float gstep_px(const GStepArgs& a, unsigned row, int 
     const size_t h0 = (size_t)rem, hR = (size_t)i * W + jp, hD = (size_t)ip * W + j;
     const float rho = a.rho[0];
     const float tau = a.lam[0] / rho;
-    const float x = a.x[P0];
-    const float xl = a.x[pb + (long long)i * W + jm], xr = a.x[PR];
-    const float xu = a.x[pb + (long long)im * W + j], xd = a.x[PD];
+    const float x = xs[P0];
+    const float xl = xs[pb + (long long)i * W + jm], xr = xs[PR];
+    const float xu = xs[pb + (long long)im * W + j], xd = xs[PD];
     const float* npx = a.nsq_prev;
     const float* npy = a.nsq_prev ? a.nsq_prev + HW : nullptr;
-    const float ux0 = gprev_u<ISO, FIRST, HIST>(a.uxi, npx, P0, h0, tau);
-    const float uxR = gprev_u<ISO, FIRST, HIST>(a.uxi, npx, PR, hR, tau);
-    const float uy0 = gprev_u<ISO, FIRST, HIST>(a.uyi, npy, P0, h0, tau);
-    const float uyD = gprev_u<ISO, FIRST, HIST>(a.uyi, npy, PD, hD, tau);
+    const float ux0 = gprev_u<ISO, FIRST, HIST>(uxs, npx, P0, h0, tau);
+    const float uxR = gprev_u<ISO, FIRST, HIST>(uxs, npx, PR, hR, tau);
+    const float uy0 = gprev_u<ISO, FIRST, HIST>(uys, npy, P0, h0, tau);
+    const float uyD = gprev_u<ISO, FIRST, HIST>(uys, npy, PD, hD, tau);
     float nx0 = 0.f, nxR = 0.f, ny0 = 0.f, nyD = 0.f;
     if constexpr (ISO) {
         nx0 = a.nsq[h0];
@@ -629,10 +633,15 @@ __device__ __forceinline__ float gstep_px(const GStepArgs& a, unsigned row, int 
     const float axR = (xr - x) + uxR, ayD = (xd - x) + uyD;
     const float zxR = shrink_z<ISO>(axR, tau, nxR), zyD = shrink_z<ISO>(ayD, tau, nyD);
     const float wxR = zxR - (axR - zxR), wyD = zyD - (ayD - zyD);
-    a.uxo[P0] = HIST ? ax : nux;
-    a.uyo[P0] = HIST ? ay : nuy;
+    uxd[P0] = HIST ? ax : nux;
+    uyd[P0] = HIST ? ay : nuy;
     const float v = (wx - wxR) + (wy - wyD);
-    return fmaf(rho, v, a.b[P0]);
+    return fmaf(rho, v, bs[P0]);
+}
+
+template <bool ISO, bool FIRST, bool HIST>
+__device__ __forceinline__ float gstep_px(const GStepArgs& a, unsigned row, int j) {
+    return gstep_pxr<ISO, FIRST, HIST>(a, a.x, a.b, a.uxi, a.uyi, a.uxo, a.uyo, row, j);
 }
 
 template <bool ISO, bool FIRST, bool HIST>
@@ -660,11 +669,18 @@ __global__ void __launch_bounds__(NT) k_grow_fwd_step(GRowArgs a, GStepArgs g) {
     const cf* tw = TWG ? a.tw : twl;
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);
-    for (int rr = 0; rr < 2 * lines; ++rr)
+    // both rows of a complex line per step: two pixels' loads in flight together
+    for (int c = 0; c < lines; ++c)
         for (int i = threadIdx.x; i < W; i += blockDim.x) {
-            const float v = rr < nl ? gstep_px<ISO, FIRST, false>(g, (unsigned)(r0 + rr), i) : 0.f;
-            float* slot = reinterpret_cast<float*>(&A[i * lines + (rr >> 1)]);
-            slot[rr & 1] = v;
+            const int rr = 2 * c;
+            float v0 = 0.f, v1 = 0.f;
+            if (rr + 1 < nl) {
+                v0 = gstep_pxr<ISO, FIRST, false>(g, g.x, g.b, g.uxi, g.uyi, g.uxo, g.uyo, (unsigned)(r0 + rr), i);
+                v1 = gstep_pxr<ISO, FIRST, false>(g, g.x, g.b, g.uxi, g.uyi, g.uxo, g.uyo, (unsigned)(r0 + rr + 1), i);
+            } else if (rr < nl) {
+                v0 = gstep_pxr<ISO, FIRST, false>(g, g.x, g.b, g.uxi, g.uyi, g.uxo, g.uyo, (unsigned)(r0 + rr), i);
+            }
+            A[i * lines + c] = mkc(v0, v1);  // even row -> real part, odd row -> imaginary part
         }
     __syncthreads();
     const cf* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
