@@ -458,7 +458,7 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
         for (int dim = 0; dim < 2; ++dim) {
             const GPlan pl = make_plan(dim == 0 ? W : H);
             if (pl.ntab == 0) continue;
-            hipLaunchKernelGGL(k_blue_tables, dim3((3 * 1024 + nt - 1) / nt), dim3(nt), 0, s,
+            hipLaunchKernelGGL(k_blue_tables, dim3((3 * 1024 * 64 + nt - 1) / nt), dim3(nt), 0, s,  // a wave per entry
                                at<cf>(ws, dim == 0 ? Lo.twW : Lo.twH), pl);
             if (int e = launch_check("k_blue_tables")) return e;
         }

@@ -365,8 +365,12 @@ __device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf
 
 // Bluestein tables of a plan, written after the n twiddles of `tab` (fp64 arithmetic, fp32 store):
 // per Bluestein stage s (R = rad[s], M = bst[s]) at tab + boff[s]: chirp[R], B[M], twM[M].
+// One wave per table entry: the M-term sum of a B entry is split over the wave's lanes (a fixed
+// lane-stride order and a fixed butterfly reduction, so the tables are deterministic); a thread
+// per entry made the setup a 100-us serial chain of 2M fp64 sincospi per B entry.
 __global__ void k_blue_tables(cf* __restrict__ tab, GPlan pl) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);  // wave-uniform
     for (int s = 0; s < pl.nst; ++s) {
         const int R = pl.rad[s], M = pl.bst[s];
         if (M == 0 || i >= R + 2 * M) continue;
@@ -375,11 +379,11 @@ __global__ void k_blue_tables(cf* __restrict__ tab, GPlan pl) {
         if (i < R) {  // c_q = exp(-i pi q^2 / R)
             const long long q2 = ((long long)i * i) % (2LL * R);
             sincospi((double)q2 / R, &im, &re);
-            o[i] = mkc((float)re, (float)-im);
+            if (lane == 0) o[i] = mkc((float)re, (float)-im);
         } else if (i < R + M) {  // B[k] = (1/M) sum_j bt_j exp(-2 pi i j k / M), bt = conj(c) even-extended
             const int k = i - R;
             double sr = 0.0, si = 0.0;
-            for (int j = 0; j < M; ++j) {
+            for (int j = lane; j < M; j += 64) {
                 const int jj = j < R ? j : (M - j < R ? M - j : -1);
                 if (jj < 0) continue;
                 const long long q2 = ((long long)jj * jj) % (2LL * R);
@@ -390,11 +394,16 @@ __global__ void k_blue_tables(cf* __restrict__ tab, GPlan pl) {
                 sr += bc * wc + bs * ws;
                 si += bs * wc - bc * ws;
             }
-            o[i] = mkc((float)(sr / M), (float)(si / M));
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                sr += __shfl_xor(sr, d, 64);
+                si += __shfl_xor(si, d, 64);
+            }
+            if (lane == 0) o[i] = mkc((float)(sr / M), (float)(si / M));
         } else {  // twM[j] = exp(-2 pi i j / M)
             const int j = i - R - M;
             sincospi(2.0 * (double)j / M, &im, &re);
-            o[i] = mkc((float)re, (float)-im);
+            if (lane == 0) o[i] = mkc((float)re, (float)-im);
         }
     }
 }
