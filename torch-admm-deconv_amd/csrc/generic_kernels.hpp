@@ -515,8 +515,15 @@ struct GColArgs {
     long long P;
 };
 
+// occupancy hint of the column pass with Bluestein stages of size 256 (waves per SIMD; A/B knob
+// -DADMM_GCOL_MINW=4 caps its VGPRs at 128)
+#ifndef ADMM_GCOL_MINW
+#define ADMM_GCOL_MINW 1
+#endif
+constexpr int gcol_minw(int bm) { return bm == 256 ? ADMM_GCOL_MINW : 1; }
+
 template <int MODE, int BM, bool TWG, int NT = GNT>
-__global__ void __launch_bounds__(NT) k_gcol(GColArgs a) {
+__global__ void __launch_bounds__(NT, gcol_minw(BM)) k_gcol(GColArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
     const int lgc = __ffs(cols) - 1;  // cols is a power of two
