@@ -61,7 +61,8 @@ def test_g7_odd_size_vs_reference(cuda_dev):
     ((1, 2, 97, 101), ("gauss:2", 7), False, 20),          # prime sizes (generic radix stages)
     ((1, 1, 360, 1000), ("motion", 15), False, 10),        # 2^3 3^2 5 x 2^3 5^3
     ((1, 1, 64, 4096), ("gauss:2", 11), False, 5),         # W beyond the fast path
-    ((1, 1, 143, 121), ("gauss:1.5", 7), True, 15),        # 11*13 x 11^2: two Bluestein stages each
+    ((1, 1, 143, 121), ("gauss:1.5", 7), True, 15),        # 11*13 x 11^2: the radix-11 / 13 butterflies
+    ((1, 2, 66, 130), ("motion", 7), False, 12),           # 2*3*11 x 2*5*13: radix 11 / 13 after other stages
     ((1, 1, 509, 37), ("motion", 9), False, 10),           # prime 509: Bluestein at M = 1024
     ((1, 2, 26, 1021), None, False, 8),                    # prime 1021 > 512: the direct prime stage
     ((1, 1, 214, 321), ("gauss:2", 7), True, 12),          # 2*107 x 3*107

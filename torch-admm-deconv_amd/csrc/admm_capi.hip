@@ -639,7 +639,8 @@ GPlan make_plan_radices(int n) {
         // 122 -> 112 ms per 250 launches, 1,410 -> 1,491 it/s)
         // (the primes >= 11 of n by trial division of n stripped of 2, 3, 5, 7: O(sqrt n))
         int r = n;
-        for (int q : {2, 3, 5, 7})
+        // (11 and 13 run as compile-time butterflies like 3, 5, 7: after the powers of two)
+        for (int q : {2, 3, 5, 7, 11, 13})
             while (r % q == 0) r /= q;
         for (int f = 11; f * f <= r; f += 2)
             if (r % f == 0) {
@@ -658,6 +659,8 @@ GPlan make_plan_radices(int n) {
         take_all(3);
         take_all(5);
         take_all(7);
+        take_all(11);
+        take_all(13);
         return p;
     }
     take_all(4);
@@ -665,7 +668,9 @@ GPlan make_plan_radices(int n) {
     take_all(3);
     take_all(5);
     take_all(7);
-    for (int f = 11; f * f <= m; f += 2) take_all(f);  // any other prime: O(R) per output
+    take_all(11);
+    take_all(13);
+    for (int f = 17; f * f <= m; f += 2) take_all(f);  // any other prime: O(R) per output
     if (m > 1) take_all(m);
     return p;
 }

@@ -70,7 +70,7 @@ __device__ __forceinline__ int fdiv(int x, int d, float rd) {
 }
 __device__ __forceinline__ float frcp(int d) { return __builtin_amdgcn_rcpf((float)d); }
 
-// cos / sin(2 pi m / R), m in [0, R), for the odd radices 3, 5, 7 (fp64 literals rounded to fp32)
+// cos / sin(2 pi m / R), m in [0, R), for the odd radices 3 ... 13 (fp64 literals rounded to fp32)
 template <int R> struct OddTw;
 template <> struct OddTw<3> {
     static constexpr double C[2] = {1.0, -0.5};
@@ -91,6 +91,23 @@ template <> struct OddTw<7> {
     static constexpr float sinv(int m) { return (float)(m <= 3 ? S[m] : -S[7 - m]); }
 };
 
+template <> struct OddTw<11> {
+    static constexpr double C[6] = {1.0, 0.8412535328311812, 0.41541501300188644, -0.142314838273285,
+                                    -0.654860733945285, -0.9594929736144974};
+    static constexpr double S[6] = {0.0, 0.5406408174555976, 0.9096319953545183, 0.9898214418809328,
+                                    0.7557495743542583, 0.28173255684142967};
+    static constexpr float cosv(int m) { return (float)C[m <= 5 ? m : 11 - m]; }
+    static constexpr float sinv(int m) { return (float)(m <= 5 ? S[m] : -S[11 - m]); }
+};
+template <> struct OddTw<13> {
+    static constexpr double C[7] = {1.0, 0.8854560256532099, 0.5680647467311559, 0.120536680255323,
+                                    -0.35460488704253545, -0.7485107481711012, -0.970941817426052};
+    static constexpr double S[7] = {0.0, 0.4647231720437685, 0.8229838658936564, 0.992708874098054,
+                                    0.9350162426854148, 0.6631226582407952, 0.23931566428755768};
+    static constexpr float cosv(int m) { return (float)C[m <= 6 ? m : 13 - m]; }
+    static constexpr float sinv(int m) { return (float)(m <= 6 ? S[m] : -S[13 - m]); }
+};
+
 template <int DIR, int R>
 __device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw, int n) {
     if constexpr (R == 2) {
@@ -106,7 +123,7 @@ __device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw,
         v[3] = csub(t1, t3);
     } else if constexpr (R == 8 || R == 16) {
         DFT<R, DIR>::template run<1, 0>(v);  // register DFT with exact constant twiddles (fft_core.hpp)
-    } else if constexpr (R == 3 || R == 5 || R == 7) {
+    } else if constexpr (R == 3 || R == 5 || R == 7 || R == 11 || R == 13) {
         // odd R with compile-time cosines / sines on the input sums / differences (the pairing of
         // gstage_any): y_k, y_{R-k} = x0 + sum_q s_q cos(qk) -+ DIR i sum_q d_q sin(qk)
         constexpr int h = (R - 1) / 2;
@@ -351,6 +368,8 @@ __device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf
                 case 16: gstage_r<DIR, 16>(src, dst, pl.n, NS, lines, tw); break;
                 case 5: gstage_r<DIR, 5>(src, dst, pl.n, NS, lines, tw); break;
                 case 7: gstage_r<DIR, 7>(src, dst, pl.n, NS, lines, tw); break;
+                case 11: gstage_r<DIR, 11>(src, dst, pl.n, NS, lines, tw); break;
+                case 13: gstage_r<DIR, 13>(src, dst, pl.n, NS, lines, tw); break;
                 default: gstage_any<DIR>(src, dst, pl.n, NS, R, lines, tw); break;
             }
         }
