@@ -361,14 +361,18 @@ def main():
     K = args.steps
     # roofline of the dominant kernel: algorithmic bytes of all its launches / its event time
     na = cnt[0]
-    bytes_a = (K * PASS_A_FIRST_BYTES + (na - K) * PASS_A_BYTES) * npx if na >= K else na * PASS_A_BYTES * npx
-    bytes_b = cnt[1] * PASS_B_BYTES * npx
+    # share of the planes one launch covers: 1, or 1/2 when a solve runs as two plane halves on two
+    # streams (the generic path's ADMM_GEN_STREAMS; the column pass runs once per iteration and half)
+    share = (K * maxit) / cnt[1] if cnt[1] > 0 else 1.0
+    bytes_a = ((K * PASS_A_FIRST_BYTES + (na * share - K) * PASS_A_BYTES) * npx if na * share >= K
+               else na * share * PASS_A_BYTES * npx)
+    bytes_b = cnt[1] * share * PASS_B_BYTES * npx
     kern = {
         "pass_a": (ms[0], na, bytes_a),
         "pass_b": (ms[1], cnt[1], bytes_b),
     }
     if iso:
-        kern["iso_norm"] = (ms[2], cnt[2], cnt[2] * ISO_NORM_BYTES * npx)
+        kern["iso_norm"] = (ms[2], cnt[2], cnt[2] * share * ISO_NORM_BYTES * npx)
     dom = max(kern, key=lambda n: kern[n][0])
     dms, dn, dbytes = kern[dom]
     achieved = (dbytes / (dms / 1e3)) / 1e9 if dms > 0 else 0.0

@@ -106,13 +106,15 @@ def test_double_backward_is_not_supported(cuda_dev):
     assert torch.equal(g1, g2)
 
 
-@pytest.mark.parametrize("iso", [False, True])
-def test_solver_is_graph_capturable(cuda_dev, iso):
+@pytest.mark.parametrize("iso,generic", [(False, False), (True, False), (False, True)])
+def test_solver_is_graph_capturable(cuda_dev, iso, generic):
     """The solve enqueues only asynchronous work on the current stream (no host synchronisation,
     workspace from the caching allocator): it can be captured in a HIP graph (torch.cuda.CUDAGraph)
     and replayed, giving the eager result bit for bit (include/admm_tv.h: graph-capturable)."""
     from admmtor.eops.deconv import fft_admm_tv
     x, k, _ = _case(cuda_dev, iso, 6)
+    if generic:  # the generic-size path (two plane halves on two streams when not captured)
+        x = x[..., :120, :250].contiguous()
     static_x = x.clone()
     eager = fft_admm_tv(static_x, 0.01, 0.02, k, iso, 12)
     s = torch.cuda.Stream(cuda_dev)
