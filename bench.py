@@ -57,6 +57,9 @@ PASS_A_BYTES = 28
 PASS_A_FIRST_BYTES = 20
 PASS_B_BYTES = 8
 ISO_NORM_BYTES = 12
+# generic sizes: the column pass (half spectra in and out, 8) and the inverse row transform that
+# follows it in the same timer (half spectra in 4, x image out 4)
+GEN_COL_BYTES = 16
 
 
 def parse():
@@ -67,6 +70,8 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="c3: skip the extra C3-at-100-iterations and C3-iso measurements after the timed region")
     ap.add_argument("--cpu-planes", type=int, default=6, help="CPU baseline sample: planes of 1024^2")
     ap.add_argument("--cpu-iters", type=int, default=36, help="CPU baseline sample: timed iterations")
     ap.add_argument("--c5-batch", type=int, default=None, help="C5 only: override the per-GPU batch")
@@ -76,25 +81,60 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(config: str, kernel: str, launches: int, steps: int):
-    """Per-launch HBM traffic of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_summary.json, made by tools/pmc/run_pmc.sh + summarize.py: separate
-    FETCH_SIZE / WRITE_SIZE passes, gfx950 corrections calibrated on the box).  None if absent."""
+def pmc_traffic(config: str, kernel: str, launches: int, steps: int, build_hash: str):
+    """Per-launch HBM traffic of `kernel` from a committed rocprofv3 PMC summary
+    (profiles/*_pmc_summary.json, made by tools/pmc/run_rdreq.sh + summarize_rdreq.py: separate
+    --pmc passes of the memory-side request-size counters) taken on THIS build: the summary records
+    the library's admm_tv_build_hash and names the kernels by role, so a summary of another build
+    (other kernels, other template arguments) is never reported.  -> (bytes or None, source)."""
     import glob
     if config not in ("c3", "c3x100"):
-        return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        summ = json.load(f)["kernels"]
-    if kernel == "pass_a":
-        first = summ.get("k_pass_a<512, false, true, false>", {}).get("traffic_bytes")
-        rest = summ.get("k_pass_a<512, false, false, false>", {}).get("traffic_bytes")
-        if first is None or rest is None or launches < steps:
-            return None, None
-        return (first * steps + rest * (launches - steps)) / launches, os.path.relpath(files[-1], ROOT)
-    return None, None
+        return None, "no PMC summary for this config"
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), reverse=True):
+        with open(path) as f:
+            summ = json.load(f)
+        if summ.get("build_hash") != build_hash or "roles" not in summ:
+            continue
+        kern, roles = summ["kernels"], summ["roles"]
+        src = os.path.relpath(path, ROOT)
+        if kernel == "pass_a":
+            first = kern.get(roles.get("pass_a_first", ""), {}).get("traffic_bytes")
+            rest = kern.get(roles.get("pass_a", ""), {}).get("traffic_bytes")
+            if first is None or rest is None or launches < steps:
+                return None, src + " (pass A roles missing)"
+            return (first * steps + rest * (launches - steps)) / launches, src
+        if kernel == "pass_b":
+            v = kern.get(roles.get("pass_b", ""), {}).get("traffic_bytes")
+            return v, src
+        return None, src
+    return None, f"no PMC summary of build {build_hash} under profiles/"
+
+
+def c3_extras(x, psf, lam, rho, no_parity, steps=3):
+    """The other C3 figures of SURVEY §8 d1, measured after the headline's timed region on the same
+    resident inputs, so one run of the default bench records them all: C3 at 100 iterations
+    (BASELINE configs[2]) with its rel-L2 vs the fp64 oracle, and C3 with block (iso) shrinkage,
+    the ADMMDeconv default.  One warm-up call, then `steps` calls between synchronisations."""
+    from admmtor.eops.deconv import fft_admm_tv
+    out = {}
+    for key, iso, maxit in (("c3_100it", False, 100), ("c3iso", True, 50)):
+        fft_admm_tv(x, lam, rho, psf, iso, maxit)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            o = fft_admm_tv(x, lam, rho, psf, iso, maxit)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        e = {"value": maxit * steps / dt, "unit": "iterations/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+             "maxit": maxit, "iso": iso, "workload": f"batch-{x.shape[0]} 1024x1024x3, 21x21 Gaussian PSF, "
+                                                     f"{'iso' if iso else 'aniso'}, {maxit} iters"}
+        if not no_parity and not iso:
+            from oracle.admm_oracle import rel_l2, solve_fourier
+            ref = solve_fourier(x[:1, :1].double().cpu(), 0.01, 0.02, psf.double().cpu(), False, maxit)
+            e["rel_l2"] = rel_l2(o[:1, :1].cpu(), ref)
+            e["rel_l2_vs"] = "fp64 CPU oracle, plane (0,0)"
+        out[key] = e
+    return out
 
 
 def cpu_baseline(cfg, planes, iters):
@@ -359,25 +399,52 @@ def main():
     P = B * C
     npx = P * H * W
     K = args.steps
-    # roofline of the dominant kernel: algorithmic bytes of all its launches / its event time
+    lib = _native.load()
+    build_hash = lib.admm_tv_build_hash().decode()
+    generic = lib.admm_tv_supported(H, W) == 2
+    # The generic aniso inference solve runs two plane halves on two streams (ADMM_GEN_STREAMS): the
+    # event times of its launches overlap and do not add up to kernel durations.  Its roofline then
+    # comes from a separate profiling pass of the same solve on one stream (after the timed region;
+    # the headline value is the timed region's).
+    two_stream = generic and not iso and P >= 2 and os.environ.get("ADMM_GEN_STREAMS", "2") != "1"
+    roof_steps, roof_note = K, "HIP events of every launch inside the timed region"
+    if two_stream:
+        roof_steps = min(K, 5)
+        os.environ["ADMM_GEN_STREAMS"] = "1"
+        try:
+            _native.profile_reset()
+            _native.profile_enable(True)
+            for _ in range(roof_steps):
+                sharded_fft_admm_tv(x, lam, rho, psf, iso, maxit)
+            torch.cuda.synchronize()
+            _native.profile_enable(False)
+            ms, cnt = _native.profile_read()
+        finally:
+            del os.environ["ADMM_GEN_STREAMS"]
+        roof_note = (f"HIP events of a one-stream profiling pass ({roof_steps} solves, ADMM_GEN_STREAMS=1) after the "
+                     "timed region: the timed solves run two plane halves on two streams, whose launches overlap")
+    # roofline of the dominant kernel: algorithmic bytes of all its launches / its event time.
+    # Fused path: pass A (row pass) and pass B (column pass).  Generic path: the row pass with the
+    # fused step (same 28 / 20 B/px) and the column pass with the inverse row transform (16 B/px).
     na = cnt[0]
-    # share of the planes one launch covers: 1, or 1/2 when a solve runs as two plane halves on two
-    # streams (the generic path's ADMM_GEN_STREAMS; the column pass runs once per iteration and half)
-    share = (K * maxit) / cnt[1] if cnt[1] > 0 else 1.0
-    bytes_a = ((K * PASS_A_FIRST_BYTES + (na * share - K) * PASS_A_BYTES) * npx if na * share >= K
-               else na * share * PASS_A_BYTES * npx)
-    bytes_b = cnt[1] * share * PASS_B_BYTES * npx
+    bytes_a = ((roof_steps * PASS_A_FIRST_BYTES + (na - roof_steps) * PASS_A_BYTES) * npx if na >= roof_steps
+               else na * PASS_A_BYTES * npx)
+    bytes_b = cnt[1] * (GEN_COL_BYTES if generic else PASS_B_BYTES) * npx
+    names = ("row_step", "column_pass") if generic else ("pass_a", "pass_b")
     kern = {
-        "pass_a": (ms[0], na, bytes_a),
-        "pass_b": (ms[1], cnt[1], bytes_b),
+        names[0]: (ms[0], na, bytes_a),
+        names[1]: (ms[1], cnt[1], bytes_b),
     }
     if iso:
-        kern["iso_norm"] = (ms[2], cnt[2], cnt[2] * share * ISO_NORM_BYTES * npx)
+        kern["iso_norm"] = (ms[2], cnt[2], cnt[2] * ISO_NORM_BYTES * npx)
     dom = max(kern, key=lambda n: kern[n][0])
     dms, dn, dbytes = kern[dom]
     achieved = (dbytes / (dms / 1e3)) / 1e9 if dms > 0 else 0.0
 
-    traffic, traffic_src = pmc_traffic(args.config, dom, dn, K)
+    traffic, traffic_src = pmc_traffic(args.config, dom, dn, roof_steps, build_hash)
+    extras = {}
+    if rank == 0 and world == 1 and args.config == "c3" and not args.no_extras:
+        extras = c3_extras(x, psf, lam, rho, args.no_parity)
     result = None
     if rank == 0:
         parity = None
@@ -392,6 +459,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg, args.cpu_planes, args.cpu_iters)
         value = world * maxit * K / T
+        it_bytes = (PASS_A_BYTES + (GEN_COL_BYTES if generic else PASS_B_BYTES) + (ISO_NORM_BYTES if iso else 0)) * npx
         result = {
             "metric": "ADMM iterations/sec, batch-64 1024x1024x3, 50 iters; rel-L2 vs CPU ref"
             if args.config == "c3" else f"ADMM iterations/sec ({args.config})",
@@ -415,18 +483,17 @@ def main():
                        if world > 1 else "shard1 (single GPU, no collective)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "build_hash": build_hash, "timing": roof_note,
                          "launches": dn, "avg_launch_ms": dms / max(dn, 1),
                          "algorithmic_bytes_per_launch": dbytes / max(dn, 1),
                          "per_kernel": {n: {"ms_total": v[0], "launches": v[1],
                                             "GBps": (v[2] / (v[0] / 1e3) / 1e9) if v[0] > 0 else None}
                                         for n, v in kern.items()}},
-            "iteration_roofline": {"bytes_per_iter": (PASS_A_BYTES + PASS_B_BYTES + (ISO_NORM_BYTES if iso else 0))
-                                   * npx, "it_s_at_peak": HBM_PEAK_GBS * 1e9 /
-                                   ((PASS_A_BYTES + PASS_B_BYTES + (ISO_NORM_BYTES if iso else 0)) * npx)},
+            "iteration_roofline": {"bytes_per_iter": it_bytes, "it_s_at_peak": HBM_PEAK_GBS * 1e9 / it_bytes},
             "parity": parity,
             "cpu_baseline": cpu,
         }
+        result.update(extras)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

@@ -14,14 +14,37 @@ def test_configs_name_the_metric_workload():
         assert len(cfg) == 9 and isinstance(cfg[8], str) and cfg[8], name
 
 
-def test_pmc_traffic_reads_committed_summary():
-    traffic, src = bench.pmc_traffic("c3", "pass_a", 490, 10)
-    if src is None:
-        pytest.skip("no committed PMC summary")
-    summ = json.load(open(os.path.join(bench.ROOT, src)))["kernels"]
-    rest = summ["k_pass_a<512, false, false, false>"]
-    assert 0.9 * rest["algorithmic_bytes"] < traffic < 1.2 * rest["algorithmic_bytes"]
-    assert bench.pmc_traffic("c2", "pass_a", 10, 1) == (None, None)
+def test_pmc_traffic_is_keyed_by_build_hash(tmp_path, monkeypatch):
+    """The roofline's traffic comes only from a PMC summary of the SAME build (its recorded
+    admm_tv_build_hash), looked up by kernel role; any other build gives traffic None."""
+    summ = {"build_hash": "abc", "workload": "c3",
+            "roles": {"pass_a_first": "k_pass_a<512, false, true, false, true>",
+                      "pass_a": "k_pass_a<512, false, false, false, true>", "pass_b": "k_pass_b<1024, 8, 0>"},
+            "kernels": {"k_pass_a<512, false, true, false, true>": {"traffic_bytes": 4.0e9},
+                        "k_pass_a<512, false, false, false, true>": {"traffic_bytes": 6.0e9},
+                        "k_pass_b<1024, 8, 0>": {"traffic_bytes": 1.7e9}}}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "r99_pmc_summary.json").write_text(json.dumps(summ))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    traffic, src = bench.pmc_traffic("c3", "pass_a", 490, 10, "abc")
+    assert src == os.path.join("profiles", "r99_pmc_summary.json")
+    assert traffic == pytest.approx((4.0e9 * 10 + 6.0e9 * 480) / 490)
+    assert bench.pmc_traffic("c3", "pass_b", 500, 10, "abc")[0] == 1.7e9
+    traffic, src = bench.pmc_traffic("c3", "pass_a", 490, 10, "other")
+    assert traffic is None and "other" in src
+    assert bench.pmc_traffic("c2", "pass_a", 10, 1, "abc")[0] is None
+
+
+def test_committed_pmc_summaries_name_their_build():
+    """Every summary bench.py may report carries the build hash and the kernel roles."""
+    import glob
+    for path in glob.glob(os.path.join(bench.ROOT, "profiles", "*_pmc_summary.json")):
+        summ = json.load(open(path))
+        if "roles" not in summ:  # rounds 1-2: never reported (no build hash)
+            continue
+        assert len(summ["build_hash"]) == 16
+        for role in ("pass_a_first", "pass_a", "pass_b"):
+            assert summ["roles"][role] in summ["kernels"], (path, role)
 
 
 def test_cpu_baseline_leg_small_sample():

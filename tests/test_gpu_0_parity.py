@@ -205,6 +205,23 @@ def test_c3_full_size_sampled(cuda_dev):
         assert e <= TOL_REF64
 
 
+@pytest.mark.slow
+def test_c2_full_size_sampled(cuda_dev):
+    """BASELINE C2 shape (32x3x512^2, 15x15 one-sided motion PSF -- non-centrosymmetric, so the
+    H_t quirk is exercised -- 50 it, aniso): the full batch runs through the W = 512 kernels
+    (16-row aniso strips, the column-pair pass B k_pass_b2); two sampled planes vs the fp64 oracle."""
+    from admmtor.synth import blurred_batch, make_psf
+    k = make_psf("motion", 15)
+    x = blurred_batch(32, 3, 512, 512, k, seed=20251206, device=cuda_dev)
+    out = solve(x, k, 0.01, 0.02, False, 50, cuda_dev)
+    assert torch.isfinite(out).all()
+    for (b, c) in ((0, 0), (31, 2)):
+        ref = oracle(x[b:b + 1, c:c + 1].cpu(), k, 0.01, 0.02, False, 50)
+        e = rel(out[b:b + 1, c:c + 1], ref)
+        print("C2 plane", b, c, e)
+        assert e <= TOL_REF64
+
+
 def test_empty_batch_and_argument_forms(cuda_dev):
     """Reference argument forms: empty batch -> empty result; lmbd / rho as floats, 1-element
     tensors (on the device or the host); negative maxit -> zeros; integer iso; float maxit."""

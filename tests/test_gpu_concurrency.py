@@ -19,10 +19,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _case(dev, iso, seed):
+def _case(dev, iso, seed, generic=False):
     from admmtor.synth import blurred_batch, make_psf
     k = make_psf("motion", 9)
     x = blurred_batch(3, 3, 128, 256, k, seed=seed).to(dev)
+    if generic:  # a generic size: the aniso inference solve runs as two plane halves on two streams
+        x = x[..., :120, :250].contiguous()
     return x, k.to(dev), iso
 
 
@@ -39,7 +41,10 @@ def _run(x, k, iso, grad):
 
 def test_two_threads_two_streams_bit_identical(cuda_dev):
     cases = [(_case(cuda_dev, False, 1), False), (_case(cuda_dev, True, 2), True),
-             (_case(cuda_dev, False, 3), True), (_case(cuda_dev, True, 4), False)]
+             (_case(cuda_dev, False, 3), True), (_case(cuda_dev, True, 4), False),
+             # generic-size aniso inference on both threads: the fork / join of the two-stream
+             # solve runs concurrently, each caller stream with its own auxiliary stream
+             (_case(cuda_dev, False, 7, True), False), (_case(cuda_dev, False, 8, True), False)]
     serial = [_run(*c, grad) for c, grad in cases]
     torch.cuda.synchronize()
     results = [[None] * len(cases) for _ in range(2)]
@@ -132,3 +137,39 @@ def test_solver_is_graph_capturable(cuda_dev, iso, generic):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(static_out, fft_admm_tv(x.flip(-1), 0.01, 0.02, k, iso, 12))
+
+
+@pytest.mark.parametrize("B,C,H,W", [(1, 3, 321, 481), (3, 1, 121, 250), (1, 2, 45, 64), (5, 3, 33, 40)])
+def test_two_stream_split_matches_one_stream(cuda_dev, monkeypatch, B, C, H, W):
+    """The generic row kernels transform real rows in pairs: the two-stream split of an aniso
+    inference solve puts an even number of rows in its first half (odd H: an even plane count), so
+    the eager two-stream solve equals the one-stream solve (ADMM_GEN_STREAMS=1, also what a
+    captured solve runs) bit for bit -- odd H with P = 3 included (the BSD image, 1x3x321x481)."""
+    from admmtor.eops.deconv import fft_admm_tv
+    from admmtor.synth import blurred_batch, make_psf
+    k = make_psf("gauss:1.5", 9)
+    x = blurred_batch(B, C, H, W, k, seed=11).to(cuda_dev)
+    two = fft_admm_tv(x, 0.01, 0.02, k.to(cuda_dev), False, 8)
+    monkeypatch.setenv("ADMM_GEN_STREAMS", "1")
+    one = fft_admm_tv(x, 0.01, 0.02, k.to(cuda_dev), False, 8)
+    torch.cuda.synchronize()
+    assert torch.equal(two, one)
+
+
+def test_input_on_another_device_than_current(cuda_dev):
+    """A solve of tensors on cuda:1 while the current device is cuda:0 runs on cuda:1: the library
+    takes the device from the caller's stream (two-stream generic solve, fused solve, backward)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two ROCm devices")
+    from admmtor.eops.deconv import fft_admm_tv
+    d1 = torch.device("cuda:1")
+    torch.cuda.set_device(0)
+    for generic in (True, False):
+        x, k, _ = _case(torch.device("cpu"), False, 9, generic)
+        ref = fft_admm_tv(x.to(cuda_dev), 0.01, 0.02, k.to(cuda_dev), False, 10).cpu()
+        out = fft_admm_tv(x.to(d1), 0.01, 0.02, k.to(d1), False, 10)
+        assert out.device == d1 and torch.cuda.current_device() == 0
+        assert torch.equal(out.cpu(), ref)
+        xg = x.to(d1).requires_grad_(True)
+        fft_admm_tv(xg, 0.01, 0.02, k.to(d1), True, 6).square().sum().backward()
+        assert xg.grad.device == d1 and torch.isfinite(xg.grad).all()

@@ -55,14 +55,49 @@ def _worker(rank, world, port, iso, q, B=5):
         dist.all_reduce(g)  # what DDP does with replicated lambda / rho
         gathered = sharded_fft_admm_tv(full[s:e], 0.02, 0.05, k, iso, 15, gather="all")
         torch.cuda.synchronize()
-
         def rel(a, b):  # an empty shard (B < world) compares nothing
             return ((a.double() - b.double()).norm() / b.double().norm()).item() if b.numel() else 0.0
+
+        side_rel = direct_rel = 0.0
+        if iso:
+            # (a) the sharded solve inside a non-default torch stream
+            st = torch.cuda.Stream(dev)
+            st.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(st):
+                side = sharded_fft_admm_tv(full[s:e], 0.02, 0.05, k, iso, 15)
+            st.synchronize()
+            # (b) the C ABI called on a side stream while torch's current stream is the default one:
+            # the hook must order its collective on the library's stream argument
+            direct = _direct_iso(full[s:e].contiguous(), k, 0.02, 0.05, 15)
+            side_rel, direct_rel = rel(side, ref[s:e].detach()), rel(direct, ref[s:e].detach())
         q.put((rank, rel(out, ref[s:e].detach()), rel(xs.grad, xr.grad[s:e]),
                rel(g[0:1], lr.grad), rel(g[1:2], rr.grad),
-               torch.equal(gathered, ref.detach()), rel(gathered, ref.detach())))
+               torch.equal(gathered, ref.detach()), rel(gathered, ref.detach()), side_rel, direct_rel))
     finally:
         dist.destroy_process_group()
+
+
+def _direct_iso(xl, k, lam, rho, maxit):
+    """admm_tv_forward through ctypes on a side stream (torch's current stream stays the default)."""
+    from admmtor import _native
+    lib = _native.load()
+    dev = k.device
+    B, C, H, W = xl.shape
+    bound = _native.AllReduceHook().bind()
+    d = _native.desc(B, C, H, W, k.shape[-1], True, maxit, 0, 1, bound)
+    ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=dev)
+    bound.add(ws)
+    out = torch.empty_like(xl)
+    lam_t = torch.tensor([lam], device=dev)
+    rho_t = torch.tensor([rho], device=dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    _native.check(lib.admm_tv_forward(d, xl.data_ptr() if xl.numel() else None, k.data_ptr(), lam_t.data_ptr(),
+                                      rho_t.data_ptr(), out.data_ptr() if out.numel() else None, ws.data_ptr(),
+                                      ws.numel(), side.cuda_stream))
+    bound.check()
+    side.synchronize()
+    return out
 
 
 @pytest.mark.parametrize("iso,B", [(False, 5), (True, 5), (True, 1)])
@@ -78,10 +113,12 @@ def test_sharded_world2_on_gpu(cuda_dev, iso, B):
     for p in procs:
         p.join(300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    for rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat in sorted(q.get(timeout=10) for _ in range(2)):
-        print("iso" if iso else "aniso", rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat)
+    for rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat, e_side, e_direct in sorted(q.get(timeout=10) for _ in range(2)):
+        print("iso" if iso else "aniso", rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat, e_side, e_direct)
         if iso:
             # fp32 reassociation only: per-pixel norms and tau^ partials summed per rank, then across
             assert e_out <= 1e-6 and e_gx <= 1e-5 and e_gl <= 5e-5 and e_gr <= 1e-4 and e_gat <= 1e-6
+            # the same solve on a non-default torch stream, and on a library stream that is not torch's
+            assert e_side <= 1e-6 and e_direct <= 1e-6
         else:
             assert bitexact and e_out == 0.0 and e_gx <= 1e-6 and e_gl <= 1e-5 and e_gr <= 1e-5

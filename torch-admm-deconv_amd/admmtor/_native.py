@@ -243,8 +243,18 @@ class BoundAllReduce:
         if self.error is not None:
             return
         try:
-            self._dist.all_reduce(self._view_of(int(ptr), int(count)), op=self._dist.ReduceOp.SUM,
-                                  group=self._group)
+            import torch
+            buf = self._view_of(int(ptr), int(count))
+            # The collective must be ordered on the stream the library queued the sums on (its
+            # `stream` argument), whatever torch's current stream is: RCCL / gloo order a
+            # collective against torch's current stream, so make that stream current for the call.
+            if buf.is_cuda:
+                st = torch.cuda.ExternalStream(int(stream), device=buf.device) if stream \
+                    else torch.cuda.default_stream(buf.device)
+                with torch.cuda.device(buf.device), torch.cuda.stream(st):
+                    self._dist.all_reduce(buf, op=self._dist.ReduceOp.SUM, group=self._group)
+            else:
+                self._dist.all_reduce(buf, op=self._dist.ReduceOp.SUM, group=self._group)
         except BaseException as e:  # noqa: BLE001 -- re-raised by check()
             self.error = e
 

@@ -95,12 +95,8 @@ def sharded_fft_admm_tv(x_local: torch.Tensor, lmbd, rho, kern: torch.Tensor, is
         return out
     if gather != "all":
         raise ValueError("gather must be None or 'all'")
-    B = total_batch
-    if B is None:
-        n = torch.tensor([x_local.shape[0]], device=x_local.device)
-        dist.all_reduce(n, group=group)
-        B = int(n.item())
-    per = -(-B // world)
+    sizes = shard_sizes(x_local.shape[0], group=group, total_batch=total_batch)
+    B, per = sum(sizes), max(sizes)
     if out.shape[0] == per:
         src = out.contiguous()
     else:  # a short shard (B not divisible by the world size) is padded to the common size
@@ -113,5 +109,39 @@ def sharded_fft_admm_tv(x_local: torch.Tensor, lmbd, rho, kern: torch.Tensor, is
         dist.all_gather(list(full.chunk(world, 0)), src, group=group)
     if per * world == B:  # equal shards: the gathered buffer is the output
         return full
-    return torch.cat([full[r * per: r * per + (shard_bounds(B, world, r)[1] - shard_bounds(B, world, r)[0])]
-                      for r in range(world)], 0)
+    return torch.cat([full[r * per: r * per + sizes[r]] for r in range(world)], 0)
+
+
+_size_groups = {}
+
+
+def _host_group(group):
+    """A CPU (gloo) process group over the same ranks as `group`, for host-side metadata: exchanging
+    shard sizes there needs no device synchronisation (an RCCL collective of a size tensor would
+    need a .item() host sync, which breaks the no-sync / graph-capturable contract of b3/b5).
+    Created once per group, collectively, on first use (every rank reaches it through the same
+    sharded_fft_admm_tv call)."""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = id(group) if group is not None else None
+    if key not in _size_groups:
+        ranks = None if group is None else dist.get_process_group_ranks(group)
+        _size_groups[key] = dist.new_group(ranks=ranks, backend="gloo")
+    return _size_groups[key]
+
+
+def shard_sizes(local: int, group=None, total_batch: Optional[int] = None):
+    """Every rank's shard size along the batch.  With `total_batch` the shards are the contiguous
+    split of shard_bounds (no communication); otherwise the sizes are exchanged on the host over
+    a CPU group (no device synchronisation), so any split -- also an uneven or empty shard -- works."""
+    world = dist.get_world_size(group)
+    if total_batch is not None:
+        sizes = [e - s for s, e in (shard_bounds(int(total_batch), world, r) for r in range(world))]
+        if sizes[dist.get_rank(group)] != local:
+            raise ValueError(f"total_batch={total_batch}: this rank holds {local} items, shard_bounds gives "
+                             f"{sizes[dist.get_rank(group)]}")
+        return sizes
+    t = torch.tensor([int(local)], dtype=torch.int64)
+    parts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(parts, t, group=_host_group(group))
+    return [int(p[0]) for p in parts]

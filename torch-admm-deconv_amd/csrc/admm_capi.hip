@@ -30,7 +30,7 @@ int fail(int code, const std::string& msg) {
 
 // ------------------------------------------------------------------ profiling
 struct ProfRec {
-    int kind;
+    int kind, dev;
     hipEvent_t a, b;
 };
 // process-wide totals (bench.py reads them); every access holds g_prof.mu, so solves on
@@ -39,29 +39,33 @@ struct Prof {
     std::mutex mu;
     bool on = false;
     std::vector<ProfRec> recs;
-    std::vector<hipEvent_t> pool;
+    std::vector<std::pair<int, hipEvent_t>> pool;  // (device, event): an event records on its device's streams
     double ms[4] = {0, 0, 0, 0};
     int64_t n[4] = {0, 0, 0, 0};
 } g_prof;
 
-hipEvent_t prof_event() {  // caller holds g_prof.mu
-    if (!g_prof.pool.empty()) {
-        hipEvent_t e = g_prof.pool.back();
-        g_prof.pool.pop_back();
-        return e;
-    }
+hipEvent_t prof_event() {  // caller holds g_prof.mu; an event of the current device
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    for (size_t i = 0; i < g_prof.pool.size(); ++i)
+        if (g_prof.pool[i].first == dev) {
+            hipEvent_t e = g_prof.pool[i].second;
+            g_prof.pool[i] = g_prof.pool.back();
+            g_prof.pool.pop_back();
+            return e;
+        }
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
     return e;
 }
 
 struct ProfScope {
-    int kind;
+    int kind, dev = 0;
     hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
     ProfScope(int k, hipStream_t st) : kind(k), s(st) {
         std::lock_guard<std::mutex> lk(g_prof.mu);
-        if (g_prof.on) {
+        if (g_prof.on && hipGetDevice(&dev) == hipSuccess) {
             a = prof_event();
             b = prof_event();
             if (a && b) (void)hipEventRecord(a, s);
@@ -71,7 +75,7 @@ struct ProfScope {
         if (a && b) {
             (void)hipEventRecord(b, s);
             std::lock_guard<std::mutex> lk(g_prof.mu);
-            g_prof.recs.push_back({kind, a, b});
+            g_prof.recs.push_back({kind, dev, a, b});
         }
     }
 };
@@ -317,25 +321,44 @@ int col_e(int H) { return H >= 1024 ? 16 : H >= 64 ? 8 : 4; }
 
 int passb_order(int H) { return std::max(1, std::min(64, env_int("ADMM_PASSB_GROUP", H >= 1024 ? 2 : 1))); }
 
+// planes per pass B block (k_pass_b gp): the block keeps its multipliers in registers across them
+// and reads the Wiener-factor table once per gp planes.  A divisor of the planes per module (a group
+// never straddles two Wiener factors).  Measured at C3 (profiles/r03_ab_passb_gp.txt): gp = 4 takes
+// pass B 0.346 -> 0.336 ms but the following pass A +1.5 % (whole iteration +-0), gp = 8 slower;
+// default 1.  ADMM_PASSB_GP (A/B knob) overrides it.
+int passb_gp(int H, int P, int ppm) {
+    (void)H;
+    int g = env_int("ADMM_PASSB_GP", 1);
+    g = std::max(1, std::min(g, 64));
+    while (g > 1 && (ppm % g)) --g;
+    (void)P;
+    return g;
+}
+
 template <int H, int C> int pass_b_hc(const cf* spec, cf* out, const float* fcT, const cf* mT, const cf* twH, int N,
                                       int P, int mode, int ppm, hipStream_t s) {
     using G = ColGeom<H, C>;
     const int colblocks = N / C;
-    const dim3 grid((unsigned)((long long)P * colblocks));
-    const int order = passb_order(H);
+    const int gp = passb_gp(H, P, ppm);
+    const dim3 grid((unsigned)((long long)((P + gp - 1) / gp) * colblocks));
+    const int order = gp > 1 ? 1 : passb_order(H);
     const int fpack = mode == 0 && env_int("ADMM_PASSB_FPACK", 1) ? 1 : 0;  // A/B knob
+    // block remap / plane order (k_pass_b pmode): contiguous XCD ranges, plane groups walked in
+    // reverse (the planes pass A wrote last first): pass B 0.3465 -> 0.3420 ms at C3, whole
+    // iteration +-0; pair-interleaved remap (4, 5) +9 % (profiles/r03_ab_passb_order.txt)
+    const int pmode = env_int("ADMM_PASSB_PMODE", 3);
     if (mode == 0) {
         if (int e = set_lds(k_pass_b<H, C, 0>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
-                           order, fpack);
+                           order, fpack, gp, P, pmode);
     } else if (mode == 1) {
         if (int e = set_lds(k_pass_b<H, C, 1>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 1>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
-                           order, fpack);
+                           order, fpack, gp, P, pmode);
     } else {
         if (int e = set_lds(k_pass_b<H, C, 2>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 2>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
-                           order, fpack);
+                           order, fpack, gp, P, pmode);
     }
     return launch_check("k_pass_b");
 }
@@ -512,13 +535,102 @@ int strip_rows(int H, int N, long long rows, bool aniso_fwd = false) {
     return R;
 }
 
-// the calling thread's auxiliary stream on the current device (created once, never destroyed)
-hipStream_t aux_stream() {
-    thread_local hipStream_t st[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    if (!st[dev] && hipStreamCreateWithFlags(&st[dev], hipStreamNonBlocking) != hipSuccess) st[dev] = nullptr;
-    return st[dev];
+// The device a call runs on is the device of its stream (the legacy default stream: the current
+// device).  Every entry point switches to it for the duration of the call and switches back, so
+// an input on cuda:1 solved while the current device is 0 launches, records and waits on device 1.
+struct DeviceGuard {
+    int prev = -1, dev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(hipStream_t s) {
+        err = hipGetDevice(&prev);
+        if (err != hipSuccess) return;
+        dev = prev;
+        if (s) {
+            hipDevice_t d = 0;
+            err = hipStreamGetDevice(s, &d);
+            if (err != hipSuccess) return;
+            dev = (int)d;
+        }
+        if (dev != prev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0 && dev != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// Auxiliary streams of the two-stream solves, one per (device, caller stream): two solves on
+// independent caller streams keep independent auxiliary streams (no false dependency between
+// them), and every thread that uses the same caller stream shares its auxiliary stream (no
+// per-thread leak).  Bounded: beyond kAuxPerDev caller streams per device the entries are reused
+// round-robin (a reused entry only adds ordering, never a hazard).  The streams live until the
+// process ends (destroying them from a static destructor could race the HIP runtime's teardown).
+struct AuxEntry {
+    hipStream_t caller = nullptr, aux = nullptr;
+};
+constexpr int kAuxDev = 64, kAuxPerDev = 32;
+struct AuxPool {
+    std::mutex mu;
+    AuxEntry e[kAuxDev][kAuxPerDev];
+    int used[kAuxDev] = {}, next[kAuxDev] = {};
+} g_aux;
+
+// the auxiliary stream paired with caller stream s on device dev (the current device, see DeviceGuard)
+hipStream_t aux_stream(hipStream_t s, int dev) {
+    if (dev < 0 || dev >= kAuxDev) return nullptr;
+    std::lock_guard<std::mutex> lk(g_aux.mu);
+    AuxEntry* row = g_aux.e[dev];
+    for (int i = 0; i < g_aux.used[dev]; ++i)
+        if (row[i].caller == s) return row[i].aux;
+    AuxEntry* slot;
+    if (g_aux.used[dev] < kAuxPerDev) {
+        slot = &row[g_aux.used[dev]];
+        if (hipStreamCreateWithFlags(&slot->aux, hipStreamNonBlocking) != hipSuccess) {
+            slot->aux = nullptr;
+            return nullptr;
+        }
+        ++g_aux.used[dev];
+    } else {
+        slot = &row[g_aux.next[dev]];
+        g_aux.next[dev] = (g_aux.next[dev] + 1) % kAuxPerDev;
+    }
+    slot->caller = s;
+    return slot->aux;
+}
+
+// fork / join of a two-stream solve: s2 starts after the work already queued on s, and s waits
+// for everything queued on s2 -- also when a half fails after the fork (the join is always issued)
+struct ForkJoin {
+    hipStream_t s, s2;
+    hipEvent_t fork = nullptr, join = nullptr;
+    hipError_t err = hipSuccess;
+    ForkJoin(hipStream_t a, hipStream_t b) : s(a), s2(b) {
+        if ((err = hipEventCreateWithFlags(&fork, hipEventDisableTiming)) != hipSuccess) return;
+        if ((err = hipEventCreateWithFlags(&join, hipEventDisableTiming)) != hipSuccess) return;
+        if ((err = hipEventRecord(fork, s)) != hipSuccess) return;
+        err = hipStreamWaitEvent(s2, fork, 0);
+    }
+    hipError_t finish() {
+        hipError_t e = hipEventRecord(join, s2);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+        return e;
+    }
+    ~ForkJoin() {
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+    }
+};
+
+// split of P planes into two halves for the generic row kernels, which transform real rows in
+// pairs (rows 2c, 2c + 1 of a launch's range): the first half must hold an even number of rows,
+// or every pair of the second half would shift and the results would differ in the last bits
+// from a one-stream solve.  0: no split.
+long long gen_split(long long P, int H) {
+    long long h = P / 2;
+    if (H & 1) {
+        h &= ~1LL;
+        if (h == 0) h = P > 2 ? 2 : 0;
+    }
+    return (h > 0 && h < P) ? h : 0;
 }
 
 // planes per chunk of the aniso inference solve (run_forward): ADMM_CHUNK_PLANES > 0 sets it,
@@ -989,22 +1101,20 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, c
     // Not under stream capture: a captured solve stays on the caller's stream.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cap));
-    if (!d.iso && !train && P >= 2 && cap == hipStreamCaptureStatusNone && env_int("ADMM_GEN_STREAMS", 2) >= 2) {
-        hipStream_t s2 = aux_stream();
+    const long long h = gen_split(P, H);
+    if (!d.iso && !train && h > 0 && cap == hipStreamCaptureStatusNone && env_int("ADMM_GEN_STREAMS", 2) >= 2) {
+        int dev = 0;
+        HIPCHK(hipGetDevice(&dev));
+        hipStream_t s2 = aux_stream(s, dev);
         if (!s2) return fail(ADMM_TV_EHIP, "auxiliary stream");
-        hipEvent_t fork, join;
-        HIPCHK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(fork, s));
-        HIPCHK(hipStreamWaitEvent(s2, fork, 0));
-        const long long h = P / 2;
+        ForkJoin fj(s, s2);
+        if (fj.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("fork: ") + hipGetErrorString(fj.err));
         int e = solve_planes(0, h, s);
         if (!e) e = solve_planes(h, P - h, s2);
-        HIPCHK(hipEventRecord(join, s2));
-        HIPCHK(hipStreamWaitEvent(s, join, 0));
-        HIPCHK(hipEventDestroy(fork));
-        HIPCHK(hipEventDestroy(join));
-        return e;
+        const hipError_t je = fj.finish();
+        if (e) return e;
+        if (je != hipSuccess) return fail(ADMM_TV_EHIP, std::string("join: ") + hipGetErrorString(je));
+        return 0;
     }
     return solve_planes(0, P, s);
 }
@@ -1143,7 +1253,8 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         {
             ProfScope ps(0, st);
             cf* tout = (keep_t && it < d.maxit) ? ht(it + 1) : cspec[1 - cur];
-            PassAArgs pa{cspec[cur], tout, cb, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, crows / R, ppm};
+            PassAArgs pa{cspec[cur], tout, cb, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R, crows / R, ppm,
+                         env_int("ADMM_PASSA_REV", 0)};
             int e = with_row(N, [&](auto ops) { return decltype(ops)::pass_a(pa, d.iso != 0, first, train, st, pl); });
             if (e) return e;
         }
@@ -1156,21 +1267,19 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     // two plane halves on two streams (the caller's and a per-thread auxiliary one), so one half's
     // pass A runs beside the other half's pass B (ADMM_STREAMS)
     if (indep && P >= 2 && env_int("ADMM_STREAMS", 1) >= 2) {
-        hipStream_t s2 = aux_stream();
+        int dev = 0;
+        HIPCHK(hipGetDevice(&dev));
+        hipStream_t s2 = aux_stream(s, dev);
         if (!s2) return fail(ADMM_TV_EHIP, "auxiliary stream");
-        hipEvent_t fork, join;
-        HIPCHK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(fork, s));
-        HIPCHK(hipStreamWaitEvent(s2, fork, 0));
+        ForkJoin fj(s, s2);
+        if (fj.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("fork: ") + hipGetErrorString(fj.err));
         const long long h = P / 2;
         int e = solve_planes(0, h, h, s);
         if (!e) e = solve_planes(h, P - h, P - h, s2);
-        HIPCHK(hipEventRecord(join, s2));
-        HIPCHK(hipStreamWaitEvent(s, join, 0));
-        HIPCHK(hipEventDestroy(fork));
-        HIPCHK(hipEventDestroy(join));
-        return e;
+        const hipError_t je = fj.finish();
+        if (e) return e;
+        if (je != hipSuccess) return fail(ADMM_TV_EHIP, std::string("join: ") + hipGetErrorString(je));
+        return 0;
     }
     const long long chunk = indep ? chunk_planes(H, W, P) : P;
     for (long long p0 = 0; p0 < P; p0 += chunk)
@@ -1354,6 +1463,8 @@ int admm_tv_forward(const admm_tv_desc* dp, const float* xin, const float* kern,
     if (int e = validate(dp)) return e;
     if (((!xin || !out) && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
         return fail(ADMM_TV_EINVAL, "null pointer argument");
+    DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
+    if (dg.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("device of the stream: ") + hipGetErrorString(dg.err));
     return run_forward(*dp, xin, kern, lam, rho, out, ws, ws_bytes, nullptr, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -1372,6 +1483,8 @@ int admm_tv_forward_train(const admm_tv_desc* dp, const float* xin, const float*
         return fail(ADMM_TV_EINVAL, "null pointer argument");
     if (dp->maxit > 0 && (!hist || hist_bytes < make_hist(*dp).total))
         return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
+    DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
+    if (dg.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("device of the stream: ") + hipGetErrorString(dg.err));
     return run_forward(*dp, xin, kern, lam, rho, out, ws, ws_bytes, dp->maxit > 0 ? hist : nullptr,
                        reinterpret_cast<hipStream_t>(stream));
 }
@@ -1389,6 +1502,8 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     if (int e = validate(dp)) return e;
     const admm_tv_desc d = *dp;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
+    if (dg.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("device of the stream: ") + hipGetErrorString(dg.err));
     if ((!gout && !participate_only(d)) || !lam || !rho || (d.kh > 0 && !kern))
         return fail(ADMM_TV_EINVAL, "null pointer argument");
     const BwdLayout BL = make_bwd_layout(d);
@@ -1540,6 +1655,8 @@ int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float*
     if (int e = validate(dp)) return e;
     const admm_tv_desc d = *dp;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
+    if (dg.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("device of the stream: ") + hipGetErrorString(dg.err));
     const Layout Lo = make_layout(d);
     if (!ws || ws_bytes < Lo.total) return fail(ADMM_TV_EWORKSPACE, "workspace too small");
     const long long P = d.B * d.C;
@@ -1570,8 +1687,8 @@ int admm_tv_profile_reset(void) {
     std::lock_guard<std::mutex> lk(g_prof.mu);
     for (auto& r : g_prof.recs) {
         (void)hipEventSynchronize(r.b);
-        g_prof.pool.push_back(r.a);
-        g_prof.pool.push_back(r.b);
+        g_prof.pool.push_back({r.dev, r.a});
+        g_prof.pool.push_back({r.dev, r.b});
     }
     g_prof.recs.clear();
     for (int i = 0; i < 4; ++i) {
@@ -1590,8 +1707,8 @@ int admm_tv_profile_read(double* ms4, int64_t* count4) {
             g_prof.ms[r.kind] += ms;
             g_prof.n[r.kind] += 1;
         }
-        g_prof.pool.push_back(r.a);
-        g_prof.pool.push_back(r.b);
+        g_prof.pool.push_back({r.dev, r.a});
+        g_prof.pool.push_back({r.dev, r.b});
     }
     g_prof.recs.clear();
     for (int i = 0; i < 4; ++i) {

@@ -314,6 +314,17 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// Pair-interleaved XCD remap: hardware block b runs on XCD b % 8 at slot b / 8; logical ids are
+// handed out so that the two blocks of a line-sharing pair (logical 2i, 2i + 1) run on the same
+// XCD in consecutive slots, and the pair index rises with the slot across all XCDs (pair 8k + x
+// on XCD x at slots 2k, 2k + 1): the launch walks its tiles in one global order instead of eight
+// ranges side by side.  Identity on the last partial group of 16.  Bijective for any nb.
+__device__ __forceinline__ unsigned xcd_pairs(unsigned b, unsigned nb) {
+    if ((b | 15u) >= nb) return b;
+    const unsigned x = b & 7u, s = b >> 3;
+    return 2u * (8u * (s >> 1) + x) + (s & 1u);
+}
+
 // block -> (plane p, column block cb) in groups of G planes (G = order; 1 = plane-major): inside a
 // group, consecutive ids are the two column blocks that share every 128-B line (PAIRS; one block
 // column for k_pass_b2, which covers whole lines), then the same columns of the group's next plane.
@@ -339,10 +350,19 @@ __device__ __forceinline__ void pb_tile(unsigned lb, int colblocks, int order, b
     }
 }
 
+#ifndef ADMM_PASSB_MHOIST
+#define ADMM_PASSB_MHOIST 1
+#endif
+// A block runs its column block through gp planes in turn (plane group pg: planes pg*gp ...; the
+// group never straddles two modules): its multipliers stay in registers and its twiddles in LDS
+// for all of them, so the Wiener-factor table is read once per gp planes instead of once per
+// plane (at C3 the per-plane reads were 0.40 GB of extra requests per launch, served by the
+// Infinity Cache, +51 % of pass B's reads).
 template <int H, int C, int MODE>
 __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCfg<H>::E), sizeof(cf) * (H + (size_t)H * C)))
     k_pass_b(const cf* spec_in, cf* spec_out, const float* __restrict__ fcT, const cf* __restrict__ mT,
-             const cf* __restrict__ twH_g, int N, int colblocks, int ppm, int order, int fpack) {
+             const cf* __restrict__ twH_g, int N, int colblocks, int ppm, int order, int fpack, int gp, int P,
+             int pmode) {
     using G = ColGeom<H, C>;
     constexpr int E = G::E, L = G::L;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -351,83 +371,100 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), pb_minw(C * (H / RowCf
     load_tw(tw, twH_g, H);
     const int tid = threadIdx.x;
     const int c = tid % C, t = tid / C;
-    int p, cb;
-    pb_tile(xcd_remap(blockIdx.x, gridDim.x), colblocks, order, true, p, cb);
+    // pmode: bits 1-2 the block remap (0 none, 1 contiguous XCD ranges, 2 pair-interleaved), bit 0
+    // walks the plane groups in reverse (the planes the previous pass wrote last come first)
+    const unsigned rb = (pmode >> 1) == 1 ? xcd_remap(blockIdx.x, gridDim.x)
+                        : (pmode >> 1) == 2 ? xcd_pairs(blockIdx.x, gridDim.x) : blockIdx.x;
+    int pg, cb;
+    pb_tile(rb, colblocks, order, true, pg, cb);
+    if (pmode & 1) pg = (int)(gridDim.x / (unsigned)colblocks) - 1 - pg;
     const int col = cb * C + c;
-    if (MODE == 0) fcT += (size_t)(p / ppm) * (N + 1) * H;  // this module's Wiener factor
-    // one plane of the spectrum = H*N*8 bytes (< 4 GiB); element (row, col) at (row*N + col)*8
-    const rsrc_t rs = make_rsrc(spec_in + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
-    const rsrc_t ro = make_rsrc(spec_out + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+    const int p0 = pg * gp;
+    if (MODE == 0) fcT += (size_t)(p0 / ppm) * (N + 1) * H;  // this module's Wiener factor
     const int voff = (t * N + col) * (int)sizeof(cf);
     const int sstep = L * N * (int)sizeof(cf);
-    cf v[E];
-#pragma unroll
-    for (int j = 0; j < E; ++j) v[j] = bload_cf<(ADMM_NT & 8) ? 2 : 0>(rs, voff, j * sstep);
-    // multipliers for this column, prefetched with the data (L2-resident tables)
     using MT = typename std::conditional<MODE == 0, float, cf>::type;
     MT m[E];
-    if (MODE == 0 && fpack) {
-        // the packed copy of the Wiener factors (k_fc_pack, after the G tables of this region): a
-        // thread's E factors are contiguous, E/4 16-byte loads instead of E 4-byte ones
-        const float* fcP = fcT + (size_t)(gridDim.x / colblocks / ppm) * (N + 1) * H;  // fcT: this module's
-        const float4* q = reinterpret_cast<const float4*>(fcP + ((size_t)col * L + t) * E);
-#pragma unroll
-        for (int j = 0; j < E / 4; ++j) {
-            const float4 f = q[j];
-            if constexpr (MODE == 0) {
-                m[4 * j] = f.x;
-                m[4 * j + 1] = f.y;
-                m[4 * j + 2] = f.z;
-                m[4 * j + 3] = f.w;
+    // multipliers of this thread's column (L2-resident tables)
+    auto load_m = [&]() {
+        if (MODE == 0 && fpack) {
+            // the packed copy of the Wiener factors (k_fc_pack, after the G tables of this region): a
+            // thread's E factors are contiguous, E/4 16-byte loads instead of E 4-byte ones
+            const float* fcP = fcT + (size_t)(P / ppm) * (N + 1) * H;  // fcT: this module's
+            const float4* qq = reinterpret_cast<const float4*>(fcP + ((size_t)col * L + t) * E);
+    #pragma unroll
+            for (int j = 0; j < E / 4; ++j) {
+                const float4 f = qq[j];
+                if constexpr (MODE == 0) {
+                    m[4 * j] = f.x;
+                    m[4 * j + 1] = f.y;
+                    m[4 * j + 2] = f.z;
+                    m[4 * j + 3] = f.w;
+                }
+            }
+        } else {
+            const rsrc_t rm = MODE == 0 ? make_rsrc(fcT, (unsigned)((size_t)(N + 1) * H * sizeof(float)))
+                                        : make_rsrc(mT, (unsigned)((size_t)(N + 1) * H * sizeof(cf)));
+            const int mo = (col * H + t) * (int)sizeof(MT);
+    #pragma unroll
+            for (int j = 0; j < E; ++j) {
+                if constexpr (MODE == 0) m[j] = bload_f(rm, mo, j * L * (int)sizeof(float));
+                else if constexpr (MODE == 1) m[j] = bload_cf(rm, mo, j * L * (int)sizeof(cf));
+                else m[j] = cconj(bload_cf(rm, mo, j * L * (int)sizeof(cf)));
             }
         }
-    } else {
-        const rsrc_t rm = MODE == 0 ? make_rsrc(fcT, (unsigned)((size_t)(N + 1) * H * sizeof(float)))
-                                    : make_rsrc(mT, (unsigned)((size_t)(N + 1) * H * sizeof(cf)));
-        const int mo = (col * H + t) * (int)sizeof(MT);
+    };
+    // ADMM_PASSB_MHOIST: load them once and keep them in registers for the gp planes (+16 VGPRs held
+    // across the forward transform), else reload them per plane
+    if (ADMM_PASSB_MHOIST) load_m();
+#pragma clang loop unroll(disable)
+    for (int q = 0; q < gp; ++q) {
+        const int p = p0 + q;
+        if (p >= P) break;  // block-uniform
+        ColBuf<C> buf{data + c};
+        // one plane of the spectrum = H*N*8 bytes (< 4 GiB); element (row, col) at (row*N + col)*8
+        const rsrc_t rs = make_rsrc(spec_in + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+        const rsrc_t ro = make_rsrc(spec_out + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+        cf v[E];
 #pragma unroll
-        for (int j = 0; j < E; ++j) {
-            if constexpr (MODE == 0) m[j] = bload_f(rm, mo, j * L * (int)sizeof(float));
-            else if constexpr (MODE == 1) m[j] = bload_cf(rm, mo, j * L * (int)sizeof(cf));
-            else m[j] = cconj(bload_cf(rm, mo, j * L * (int)sizeof(cf)));
-        }
-    }
-    __syncthreads();
-    ColBuf<C> buf{data + c};
-    fft<H, L, -1, 1, 1>(v, buf, tw, t);
-    if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H-ky]
-        __syncthreads();
+        for (int j = 0; j < E; ++j) v[j] = bload_cf<(ADMM_NT & 8) ? 2 : 0>(rs, voff, j * sstep);
+        if (!ADMM_PASSB_MHOIST) load_m();  // per plane (L2 hits after the group's first plane)
+        __syncthreads();  // q = 0: the twiddles are in LDS; q > 0: the previous plane's LDS reads are done
+        fft<H, L, -1, 1, 1>(v, buf, tw, t);
+        if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H-ky]
+            __syncthreads();
 #pragma unroll
-        for (int j = 0; j < E; ++j) buf.at(t + L * j) = v[j];
-        __syncthreads();
-        if (col == 0) {
+            for (int j = 0; j < E; ++j) buf.at(t + L * j) = v[j];
+            __syncthreads();
+            if (col == 0) {
 #pragma unroll
-            for (int j = 0; j < E; ++j) {
-                const int ky = t + L * j;
-                const cf q = cconj(buf.at((H - ky) & (H - 1)));
-                if constexpr (MODE == 0) {
-                    const float f0 = m[j], fn = fcT[(size_t)N * H + ky];
-                    const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
-                    v[j] = mkc(fmaf(a, v[j].x, b * q.x), fmaf(a, v[j].y, b * q.y));
-                } else {
-                    const cf m0 = m[j], mn = MODE == 1 ? mT[(size_t)N * H + ky] : cconj(mT[(size_t)N * H + ky]);
-                    const cf a = mkc(0.5f * (m0.x + mn.x), 0.5f * (m0.y + mn.y));
-                    const cf b = mkc(0.5f * (m0.x - mn.x), 0.5f * (m0.y - mn.y));
-                    v[j] = cadd(cmul(v[j], a), cmul(q, b));
+                for (int j = 0; j < E; ++j) {
+                    const int ky = t + L * j;
+                    const cf qv = cconj(buf.at((H - ky) & (H - 1)));
+                    if constexpr (MODE == 0) {
+                        const float f0 = m[j], fn = fcT[(size_t)N * H + ky];
+                        const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
+                        v[j] = mkc(fmaf(a, v[j].x, b * qv.x), fmaf(a, v[j].y, b * qv.y));
+                    } else {
+                        const cf m0 = m[j], mn = MODE == 1 ? mT[(size_t)N * H + ky] : cconj(mT[(size_t)N * H + ky]);
+                        const cf a = mkc(0.5f * (m0.x + mn.x), 0.5f * (m0.y + mn.y));
+                        const cf b = mkc(0.5f * (m0.x - mn.x), 0.5f * (m0.y - mn.y));
+                        v[j] = cadd(cmul(v[j], a), cmul(qv, b));
+                    }
                 }
             }
         }
-    }
-    if (col != 0) {
+        if (col != 0) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) {
-            if constexpr (MODE == 0) v[j] = cscale(v[j], m[j]);
-            else v[j] = cmul(v[j], m[j]);
+            for (int j = 0; j < E; ++j) {
+                if constexpr (MODE == 0) v[j] = cscale(v[j], m[j]);
+                else v[j] = cmul(v[j], m[j]);
+            }
         }
-    }
-    fft<H, L, +1, 1, 1>(v, buf, tw, t);
+        fft<H, L, +1, 1, 1>(v, buf, tw, t);
 #pragma unroll
-    for (int j = 0; j < E; ++j) bstore_cf<(ADMM_NT & 4) ? 2 : 0>(ro, voff, j * sstep, v[j]);
+        for (int j = 0; j < E; ++j) bstore_cf<(ADMM_NT & 4) ? 2 : 0>(ro, voff, j * sstep, v[j]);
+    }
 }
 
 // Pass B (MODE 0) with two adjacent columns per thread: 16-byte loads and stores, so the 8
@@ -562,6 +599,7 @@ struct PassAArgs {
     long long ppm;        // planes per module: with several modules solved together (desc.groups),
                           // module m = plane / ppm has lam[m], rho[m], norms at nsq + m 2HW, and
                           // all modules share b (b has ppm planes)
+    int rev = 0;          // 1: walk the strips from the last one (ADMM_PASSA_REV, A/B)
 };
 
 // occupancy target of the row pass (waves per SIMD): 3 for rows up to W = 1024 (fits
@@ -610,8 +648,9 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
 #endif
     constexpr bool kRemap = ADMM_PASSA_REMAP < 0 ? N <= 256 : ADMM_PASSA_REMAP != 0;
     const unsigned blk = kRemap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const long long strip = (long long)blk * G::SG + sgl;
+    long long strip = (long long)blk * G::SG + sgl;
     if (strip >= a.nstrips) return;
+    if (a.rev) strip = a.nstrips - 1 - strip;
     const int H = a.H, R = a.R;
     const int spp = H / R;
     const long long p = strip / spp;
