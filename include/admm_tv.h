@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ADMM_TV_ABI_VERSION 4
+#define ADMM_TV_ABI_VERSION 5
 
 enum {
     ADMM_TV_OK = 0,
@@ -84,6 +84,13 @@ typedef struct admm_tv_desc {
 /* flags: the training forward also keeps the spectra of every r_k so that
  * admm_tv_backward can form the PSF gradient (history grows by 4 B/pixel/iteration). */
 #define ADMM_TV_FLAG_PSF_GRAD 1
+/* flags: fp64 solve.  The reference computes in xin.dtype (deconv.py:49,61-67,104-106), so fp64
+ * callers get fp64 arithmetic: every array of the *_f64 entry points below is double (input, PSF,
+ * lambda, rho, output, gradients; the all-reduce hook's buffer holds `count` doubles), and the
+ * size queries (admm_tv_workspace_size, admm_tv_history_size, admm_tv_backward_workspace_size)
+ * return the fp64 sizes.  fp64 solves run on the generic (any-size) kernels' double instantiation at
+ * every H, W that admm_tv_supported_f64 accepts; groups must be 0 or 1. */
+#define ADMM_TV_FLAG_F64 2
 
 /* ABI version (ADMM_TV_ABI_VERSION). */
 int admm_tv_abi_version(void);
@@ -99,6 +106,10 @@ const char* admm_tv_build_hash(void);
  * 0: unsupported. */
 int admm_tv_supported(int64_t H, int64_t W);
 
+/* 1 when an fp64 solve (ADMM_TV_FLAG_F64) of (H, W) is supported: every line of each dimension fits
+ * the double kernels' LDS image (up to 10,240 points; 0 otherwise). */
+int admm_tv_supported_f64(int64_t H, int64_t W);
+
 /* Workspace bytes needed by admm_tv_forward for `desc`. */
 int admm_tv_workspace_size(const admm_tv_desc* desc, size_t* bytes);
 
@@ -110,6 +121,21 @@ int admm_tv_workspace_size(const admm_tv_desc* desc, size_t* bytes);
 int admm_tv_forward(const admm_tv_desc* desc, const float* xin, const float* kern,
                     const float* lambda_dev, const float* rho_dev, float* out,
                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* fp64 variants (desc->flags must hold ADMM_TV_FLAG_F64; the plain entry points refuse it): the
+ * same contracts as admm_tv_forward / admm_tv_forward_train / admm_tv_backward with double arrays. */
+int admm_tv_forward_f64(const admm_tv_desc* desc, const double* xin, const double* kern,
+                        const double* lambda_dev, const double* rho_dev, double* out,
+                        void* workspace, size_t workspace_bytes, void* stream);
+int admm_tv_forward_train_f64(const admm_tv_desc* desc, const double* xin, const double* kern,
+                              const double* lambda_dev, const double* rho_dev, double* out,
+                              void* hist, size_t hist_bytes,
+                              void* workspace, size_t workspace_bytes, void* stream);
+int admm_tv_backward_f64(const admm_tv_desc* desc, const double* xin, const double* kern,
+                         const double* lambda_dev, const double* rho_dev, const double* gout,
+                         const void* hist, size_t hist_bytes,
+                         double* gxin, double* glam, double* grho, double* gkern,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- autograd
  * Replaces the reference's implicit autograd through the unrolled loop

@@ -49,7 +49,7 @@ def test_library_is_gfx950_code():
 def test_host_entry_points():
     from admmtor import _native
     lib = _native.load()
-    assert lib.admm_tv_abi_version() == 4
+    assert lib.admm_tv_abi_version() == 5
     fast, generic = 1, 2
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
     assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 4096), (8, 64), (1, 1), (481, 321))] == [generic] * 5
@@ -61,6 +61,31 @@ def test_host_entry_points():
     assert 7 * img <= ws <= 7 * img + (64 << 20)  # 2 spectra + 4 u + b (+ small tables)
     d_iso = _native.desc(16, 3, 512, 512, 0, True, 100)
     assert _native.workspace_size(d_iso) > 6 * 16 * 3 * 512 * 512 * 4
+
+
+def test_host_entry_points_f64():
+    """fp64 solves (ADMM_TV_FLAG_F64): every size the double kernels' LDS image admits, fp64 sizes,
+    and the precision of a descriptor and of an entry point must agree."""
+    from admmtor import _native
+    lib = _native.load()
+    assert [lib.admm_tv_supported_f64(*hw) for hw in ((1024, 1024), (15, 17), (1, 1), (481, 321), (256, 4096))] \
+        == [1] * 5
+    assert [lib.admm_tv_supported_f64(*hw) for hw in ((10241, 16), (0, 16))] == [0] * 2
+    d32 = _native.desc(2, 3, 64, 96, 5, False, 10)
+    d64 = _native.desc(2, 3, 64, 96, 5, False, 10, f64=True)
+    assert d64.flags & _native.ADMM_TV_FLAG_F64
+    img = 2 * 3 * 64 * 96
+    assert _native.workspace_size(d64) >= 7 * img * 8 > _native.workspace_size(d32)
+    assert _native.history_size(_native.desc(2, 3, 64, 96, 5, False, 10, f64=True)) == \
+        2 * _native.history_size(_native.desc(2, 3, 64, 96, 5, False, 10))
+    # an fp32 entry point refuses an fp64 descriptor (and vice versa) before touching any pointer
+    assert lib.admm_tv_forward(ctypes.byref(d64), None, None, None, None, None, None, 0, None) == _native.ADMM_TV_EINVAL
+    assert lib.admm_tv_forward_f64(ctypes.byref(d32), None, None, None, None, None, None, 0, None) == \
+        _native.ADMM_TV_EINVAL
+    assert b"f64" in lib.admm_tv_last_error()
+    dg = _native.desc(2, 3, 64, 64, 0, False, 10, groups=2, f64=True)
+    n = ctypes.c_size_t(0)
+    assert lib.admm_tv_workspace_size(ctypes.byref(dg), ctypes.byref(n)) == _native.ADMM_TV_EUNSUPPORTED
 
 
 @pytest.mark.parametrize("field,value,code", [

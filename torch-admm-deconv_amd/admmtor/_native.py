@@ -27,8 +27,12 @@ EXPORTED = (
     "admm_tv_abi_version",
     "admm_tv_build_hash",
     "admm_tv_supported",
+    "admm_tv_supported_f64",
     "admm_tv_workspace_size",
     "admm_tv_forward",
+    "admm_tv_forward_f64",
+    "admm_tv_forward_train_f64",
+    "admm_tv_backward_f64",
     "admm_tv_psf_transpose",
     "admm_tv_history_size",
     "admm_tv_forward_train",
@@ -74,7 +78,8 @@ class AdmmTvDesc(ctypes.Structure):
 
 
 ADMM_TV_FLAG_PSF_GRAD = 1
-ABI_VERSION = 4
+ADMM_TV_FLAG_F64 = 2  # fp64 solve: the *_f64 entry points, double arrays
+ABI_VERSION = 5
 
 
 class NativeError(RuntimeError):
@@ -129,18 +134,23 @@ def load() -> ctypes.CDLL:
         L.admm_tv_build_hash.argtypes = []
         L.admm_tv_supported.restype = ctypes.c_int
         L.admm_tv_supported.argtypes = [ctypes.c_int64, ctypes.c_int64]
+        L.admm_tv_supported_f64.restype = ctypes.c_int
+        L.admm_tv_supported_f64.argtypes = [ctypes.c_int64, ctypes.c_int64]
         L.admm_tv_workspace_size.restype = ctypes.c_int
         L.admm_tv_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
-        L.admm_tv_forward.restype = ctypes.c_int
-        L.admm_tv_forward.argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp]
+        for f in ("admm_tv_forward", "admm_tv_forward_f64"):
+            getattr(L, f).restype = ctypes.c_int
+            getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp]
         L.admm_tv_history_size.restype = ctypes.c_int
         L.admm_tv_history_size.argtypes = [dp, ctypes.POINTER(sz)]
-        L.admm_tv_forward_train.restype = ctypes.c_int
-        L.admm_tv_forward_train.argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp]
+        for f in ("admm_tv_forward_train", "admm_tv_forward_train_f64"):
+            getattr(L, f).restype = ctypes.c_int
+            getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp]
         L.admm_tv_backward_workspace_size.restype = ctypes.c_int
         L.admm_tv_backward_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
-        L.admm_tv_backward.restype = ctypes.c_int
-        L.admm_tv_backward.argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, sz, vp]
+        for f in ("admm_tv_backward", "admm_tv_backward_f64"):
+            getattr(L, f).restype = ctypes.c_int
+            getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, sz, vp]
         L.admm_tv_psf_transpose.restype = ctypes.c_int
         L.admm_tv_psf_transpose.argtypes = [dp, vp, vp, vp, vp, sz, vp]
         L.admm_tv_profile_enable.restype = ctypes.c_int
@@ -182,10 +192,17 @@ def check(code: int) -> None:
         raise NativeError(code, msg)
 
 
-def desc(B, C, H, W, k, iso, maxit, flags=0, groups=1, allreduce=None) -> AdmmTvDesc:
-    """allreduce: a BoundAllReduce (AllReduceHook.bind) for iso over a sharded batch, or None."""
-    return AdmmTvDesc(int(B), int(C), int(H), int(W), int(k), int(k), int(bool(iso)), int(maxit), int(flags),
+def desc(B, C, H, W, k, iso, maxit, flags=0, groups=1, allreduce=None, f64=False) -> AdmmTvDesc:
+    """allreduce: a BoundAllReduce (AllReduceHook.bind) for iso over a sharded batch, or None.
+    f64: an fp64 solve (ADMM_TV_FLAG_F64; the *_f64 entry points)."""
+    flags = int(flags) | (ADMM_TV_FLAG_F64 if f64 else 0)
+    return AdmmTvDesc(int(B), int(C), int(H), int(W), int(k), int(k), int(bool(iso)), int(maxit), flags,
                       int(groups), allreduce.cfn if allreduce is not None else ALLREDUCE_FN(), None)
+
+
+def entry(name: str, f64: bool):
+    """The C entry point `name` of the solve's precision (admm_tv_forward / admm_tv_forward_f64 ...)."""
+    return getattr(load(), name + ("_f64" if f64 else ""))
 
 
 def workspace_size(d: AdmmTvDesc) -> int:
@@ -206,7 +223,9 @@ def backward_workspace_size(d: AdmmTvDesc) -> int:
     return int(n.value)
 
 
-def supported(H: int, W: int) -> bool:
+def supported(H: int, W: int, f64: bool = False) -> bool:
+    if f64:
+        return bool(load().admm_tv_supported_f64(int(H), int(W)))
     return bool(load().admm_tv_supported(int(H), int(W)))
 
 
@@ -218,8 +237,9 @@ class BoundAllReduce:
     several threads / streams each carry their own.  A Python exception inside the callback
     cannot cross the C frame: it is kept and re-raised by check() after the call returns."""
 
-    def __init__(self, dist, group, tensors=()):
+    def __init__(self, dist, group, tensors=(), f64=False):
         self._dist, self._group = dist, group
+        self._f64 = f64  # an fp64 solve hands `count` doubles
         self._bufs = []
         self.add(*tensors)
         self.error = None
@@ -231,12 +251,13 @@ class BoundAllReduce:
 
     def _view_of(self, ptr: int, count: int):
         import torch
-        nbytes = 4 * count
+        dt = torch.float64 if self._f64 else torch.float32
+        nbytes = (8 if self._f64 else 4) * count
         for t in self._bufs:
             base = t.data_ptr()
             if base <= ptr and ptr + nbytes <= base + t.numel() * t.element_size():
                 off = ptr - base
-                return t.view(torch.uint8)[off:off + nbytes].view(torch.float32)
+                return t.view(torch.uint8)[off:off + nbytes].view(dt)
         raise RuntimeError("admmtor: all-reduce buffer not inside this call's workspace")
 
     def _call(self, ptr, count, stream, ctx):
@@ -272,8 +293,8 @@ class AllReduceHook:
         self._dist = dist
         self._group = group
 
-    def bind(self, *tensors) -> BoundAllReduce:
-        return BoundAllReduce(self._dist, self._group, tensors)
+    def bind(self, *tensors, f64: bool = False) -> BoundAllReduce:
+        return BoundAllReduce(self._dist, self._group, tensors, f64=f64)
 
 
 def profile_enable(on: bool) -> None:

@@ -13,8 +13,9 @@ graph, with no graph break, and the autograd formula is registered on the op its
                             need_x, need_s, need_k) -> (gx, glam, grho, gkern)
       admm_tv_backward; gradients that are not needed come back as empty tensors
 
-All tensor arguments are fp32, contiguous, on one ROCm device (the public wrapper in
-``admmtor.eops.deconv`` stages host / fp64 / half inputs).  The backward op has no autograd
+All tensor arguments share one dtype -- fp32, or fp64 for an fp64 solve (ADMM_TV_FLAG_F64: the
+reference computes in xin.dtype, so fp64 inputs get fp64 arithmetic) -- and are contiguous, on one
+ROCm device (the public wrapper in ``admmtor.eops.deconv`` stages host / half inputs).  The backward op has no autograd
 formula of its own: differentiating the gradient again (``create_graph=True`` then a second
 ``backward``) raises PyTorch's "no autograd formula" error — double backward is not supported
 (the reference's unrolled ATen graph would allow it).  The cross-rank all-reduce hook of the
@@ -37,9 +38,20 @@ def _k(kern: Tensor) -> int:
     return int(kern.shape[-1]) if kern.numel() > 0 else 0
 
 
+def _f64(x: Tensor) -> bool:
+    return x.dtype == torch.float64
+
+
 def _desc(x: Tensor, lam: Tensor, kern: Tensor, iso: bool, maxit: int, flags: int = 0):
     B, C, H, W = x.shape
-    return _native.desc(B, C, H, W, _k(kern), iso, maxit, flags, lam.numel())
+    return _native.desc(B, C, H, W, _k(kern), iso, maxit, flags, lam.numel(), f64=_f64(x))
+
+
+def _check_supported(H: int, W: int, f64: bool) -> None:
+    if not _native.supported(H, W, f64):
+        raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported"
+                                  f"{'_f64' if f64 else ''}: any size whose lines fit the generic kernels' LDS, "
+                                  "up to 10,240)")
 
 
 def _flags(kern: Tensor, psf_grad: bool) -> int:
@@ -61,16 +73,13 @@ def _check_device(*ts: Tensor) -> None:
 def fft_admm_tv_fwd(x: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso: bool, maxit: int) -> Tensor:
     """admm_tv_forward (include/admm_tv.h) -- replaces fft_admm_tv's loop (deconv.py:35-117)."""
     _check_device(x, lam, rho, kern)
-    lib = _native.load()
     B, C, H, W = x.shape
-    if not _native.supported(H, W):
-        raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
-                                  "size whose lines fit the generic kernels' LDS, up to 10,240)")
+    _check_supported(H, W, _f64(x))
     d = _desc(x, lam, kern, iso, maxit)
     x, lam, rho, kern = x.contiguous(), lam.contiguous(), rho.contiguous(), kern.contiguous()
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x.device)
-    out = torch.empty((lam.numel() * B, C, H, W), dtype=torch.float32, device=x.device)
-    _native.check(lib.admm_tv_forward(
+    out = torch.empty((lam.numel() * B, C, H, W), dtype=x.dtype, device=x.device)
+    _native.check(_native.entry("admm_tv_forward", _f64(x))(
         d, x.data_ptr(), kern.data_ptr() if _k(kern) > 0 else None, lam.data_ptr(), rho.data_ptr(),
         out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(x.device)))
     return out
@@ -79,7 +88,7 @@ def fft_admm_tv_fwd(x: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso: bool
 @fft_admm_tv_fwd.register_fake
 def _(x, lam, rho, kern, iso, maxit):
     B, C, H, W = x.shape
-    return x.new_empty((lam.shape[0] * B, C, H, W), dtype=torch.float32)
+    return x.new_empty((lam.shape[0] * B, C, H, W), dtype=x.dtype)
 
 
 # ---------------------------------------------------------------- training forward + backward
@@ -93,17 +102,14 @@ def fft_admm_tv_fwd_train(x: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso
     """admm_tv_forward_train: the solve plus the history its backward reads (a_k per iteration,
     iso norms, and with psf_grad the r_k spectra)."""
     _check_device(x, lam, rho, kern)
-    lib = _native.load()
     B, C, H, W = x.shape
-    if not _native.supported(H, W):
-        raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
-                                  "size whose lines fit the generic kernels' LDS, up to 10,240)")
+    _check_supported(H, W, _f64(x))
     d = _desc(x, lam, kern, iso, maxit, _flags(kern, psf_grad))
     x, lam, rho, kern = x.contiguous(), lam.contiguous(), rho.contiguous(), kern.contiguous()
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x.device)
     hist = torch.empty(max(_native.history_size(d), 1), dtype=torch.uint8, device=x.device)
-    out = torch.empty((lam.numel() * B, C, H, W), dtype=torch.float32, device=x.device)
-    _native.check(lib.admm_tv_forward_train(
+    out = torch.empty((lam.numel() * B, C, H, W), dtype=x.dtype, device=x.device)
+    _native.check(_native.entry("admm_tv_forward_train", _f64(x))(
         d, x.data_ptr(), kern.data_ptr() if _k(kern) > 0 else None, lam.data_ptr(), rho.data_ptr(),
         out.data_ptr(), hist.data_ptr(), hist.numel(), ws.data_ptr(), ws.numel(), _stream(x.device)))
     return out, hist
@@ -113,10 +119,11 @@ def fft_admm_tv_fwd_train(x: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso
 def _(x, lam, rho, kern, iso, maxit, psf_grad):
     B, C, H, W = x.shape
     G = lam.shape[0]
-    out = x.new_empty((G * B, C, H, W), dtype=torch.float32)
+    out = x.new_empty((G * B, C, H, W), dtype=x.dtype)
     k = kern.shape[-1] if kern.numel() > 0 else 0
     if _is_concrete(B, C, H, W, G, k):
-        n = max(_native.history_size(_native.desc(B, C, H, W, k, iso, maxit, _flags(kern, psf_grad), G)), 1)
+        n = max(_native.history_size(_native.desc(B, C, H, W, k, iso, maxit, _flags(kern, psf_grad), G,
+                                                  f64=_f64(x))), 1)
     else:  # symbolic shapes: the history size is a closed form of the native planner, opaque here
         n = torch.library.get_ctx().new_dynamic_size()
     return out, x.new_empty((n,), dtype=torch.uint8)
@@ -128,7 +135,7 @@ def fft_admm_tv_bwd(gout: Tensor, x: Tensor, lam: Tensor, rho: Tensor, kern: Ten
                     need_k: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """admm_tv_backward: (dL/dx, dL/dlam, dL/drho, dL/dkern) from dL/dout and the history."""
     _check_device(gout, x, lam, rho, kern, hist)
-    lib = _native.load()
+    f64 = lam.dtype == torch.float64
     G = lam.numel()
     GB, C, H, W = gout.shape
     B = GB // G
@@ -138,17 +145,18 @@ def fft_admm_tv_bwd(gout: Tensor, x: Tensor, lam: Tensor, rho: Tensor, kern: Ten
         raise RuntimeError("admmtor: PSF gradient requested but the forward did not keep the spectra")
     if flags and tuple(x.shape) != (B, C, H, W):
         raise RuntimeError("admm_hip::fft_admm_tv_bwd: the PSF gradient needs the forward's input x")
-    d = _native.desc(B, C, H, W, k, iso, maxit, flags, G)
+    d = _native.desc(B, C, H, W, k, iso, maxit, flags, G, f64=f64)
     dev = gout.device
-    g = gout.contiguous()
-    e = torch.empty(0, dtype=torch.float32, device=dev)
-    gx = torch.empty((B, C, H, W), dtype=torch.float32, device=dev) if need_x else e
-    gl = torch.empty(G, dtype=torch.float32, device=dev) if need_s else e.clone()
-    gr = torch.empty(G, dtype=torch.float32, device=dev) if need_s else e.clone()
-    gk = torch.empty((1, 1, k, k), dtype=torch.float32, device=dev) if (need_k and k > 0) else e.clone()
+    dt = lam.dtype
+    g = gout.contiguous().to(dt)
+    e = torch.empty(0, dtype=dt, device=dev)
+    gx = torch.empty((B, C, H, W), dtype=dt, device=dev) if need_x else e
+    gl = torch.empty(G, dtype=dt, device=dev) if need_s else e.clone()
+    gr = torch.empty(G, dtype=dt, device=dev) if need_s else e.clone()
+    gk = torch.empty((1, 1, k, k), dtype=dt, device=dev) if (need_k and k > 0) else e.clone()
     ws = torch.empty(_native.backward_workspace_size(d), dtype=torch.uint8, device=dev)
     xc = x.contiguous() if flags else None
-    _native.check(lib.admm_tv_backward(
+    _native.check(_native.entry("admm_tv_backward", f64)(
         d, xc.data_ptr() if flags else None, kern.contiguous().data_ptr() if k > 0 else None,
         lam.contiguous().data_ptr(), rho.contiguous().data_ptr(), g.data_ptr(), hist.data_ptr(), hist.numel(),
         gx.data_ptr() if need_x else None, gl.data_ptr() if need_s else None,
@@ -164,7 +172,7 @@ def _(gout, x, lam, rho, kern, hist, iso, maxit, psf_grad, need_x, need_s, need_
     B = GB // G
     k = kern.shape[-1] if kern.numel() > 0 else 0
     def mk(shape):
-        return gout.new_empty(shape, dtype=torch.float32)
+        return gout.new_empty(shape, dtype=lam.dtype)
     gx = mk((B, C, H, W)) if need_x else mk((0,))
     gl = mk((G,)) if need_s else mk((0,))
     gr = mk((G,)) if need_s else mk((0,))

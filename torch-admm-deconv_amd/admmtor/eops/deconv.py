@@ -97,21 +97,22 @@ def _check_inputs(xin: torch.Tensor, kern: torch.Tensor):
             raise RuntimeError(f"expected kern dtype {xin.dtype}, got {kern.dtype}")
 
 
-def _as_device_scalar(v, device) -> torch.Tensor:
+def _as_device_scalar(v, device, dtype=torch.float32) -> torch.Tensor:
     if isinstance(v, torch.Tensor):
         if v.numel() != 1:
             raise NotImplementedError("lmbd / rho must be scalars or 1-element tensors")
-        return v.detach().reshape(1).to(device=device, dtype=torch.float32)
-    return torch.full((1,), float(v), dtype=torch.float32, device=device)
+        return v.detach().reshape(1).to(device=device, dtype=dtype)
+    return torch.full((1,), float(v), dtype=dtype, device=device)
 
 
-def _scalar_input(v, device) -> torch.Tensor:
-    """lmbd / rho -> fp32 (1,) device tensor; differentiable when v is a tensor that requires grad."""
+def _scalar_input(v, device, dtype=torch.float32) -> torch.Tensor:
+    """lmbd / rho -> (1,) device tensor of the solve's dtype; differentiable when v is a tensor that
+    requires grad."""
     if isinstance(v, torch.Tensor):
         if v.numel() != 1:
             raise NotImplementedError("lmbd / rho must be scalars or 1-element tensors")
-        return v.reshape(1).to(device=device, dtype=torch.float32)
-    return torch.full((1,), float(v), dtype=torch.float32, device=device)
+        return v.reshape(1).to(device=device, dtype=dtype)
+    return torch.full((1,), float(v), dtype=dtype, device=device)
 
 
 def _rocm_device() -> torch.device:
@@ -134,26 +135,26 @@ def _stage(xin, lmbd, rho, kern):
 
 def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.Tensor, iso: bool, maxit: int,
            hook=None):
-    """Run the HIP solver: x32 (B,C,H,W) fp32 contiguous on the device -> new tensor.
-    Without a hook this is the dispatcher op admm_hip::fft_admm_tv_fwd (admmtor._ops).
+    """Run the HIP solver: x32 (B,C,H,W) fp32 (or fp64: an fp64 solve) contiguous on the device -> new
+    tensor.  Without a hook this is the dispatcher op admm_hip::fft_admm_tv_fwd (admmtor._ops).
     `hook`: an _native.AllReduceHook for iso over a batch sharded across ranks; its callback is
     bound to this call's workspace only (no process-global state)."""
     if hook is None or not iso:
         return torch.ops.admm_hip.fft_admm_tv_fwd(x32, lam, rho, k32, bool(iso), int(maxit))
-    lib = _native.load()
+    f64 = x32.dtype == torch.float64
     B, C, H, W = x32.shape
     G = lam.numel()  # modules solved together (fft_admm_tv_grouped); 1 for fft_admm_tv
     k = int(k32.shape[-1]) if k32.numel() > 0 else 0
-    bound = hook.bind()
-    d = _native.desc(B, C, H, W, k, iso, maxit, 0, G, bound)
-    if not _native.supported(H, W):
+    bound = hook.bind(f64=f64)
+    d = _native.desc(B, C, H, W, k, iso, maxit, 0, G, bound, f64=f64)
+    if not _native.supported(H, W, f64):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
                                   "size whose lines fit the generic kernels' LDS, up to 10,240)")
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
     bound.add(ws)
-    out = torch.empty((G * B, C, H, W), dtype=torch.float32, device=x32.device)
+    out = torch.empty((G * B, C, H, W), dtype=x32.dtype, device=x32.device)
     stream = torch.cuda.current_stream(x32.device).cuda_stream
-    _native.check(lib.admm_tv_forward(
+    _native.check(_native.entry("admm_tv_forward", f64)(
         d, x32.data_ptr(), k32.data_ptr() if k > 0 else None, lam.data_ptr(), rho.data_ptr(),
         out.data_ptr(), ws.data_ptr(), ws.numel(), stream))
     bound.check()
@@ -174,10 +175,10 @@ def fft_admm_tv(xin: torch.Tensor,
     shrinkage, ``tau = lmbd / rho``, ``maxit`` iterations from zero, returns the
     last x with xin's shape, on xin's device.  The solve always runs as HIP kernels on a ROCm
     device: host tensors are staged to the current device and the result copied back
-    (autograd flows through both copies).  Arithmetic is fp32: fp32 inputs return fp32, fp64
-    inputs return fp64 (computed in fp32, within 1e-5 relative L2 of the reference's fp64
-    result), bf16/fp16 under ``torch.autocast`` compute in fp32 and return fp32, as the
-    reference does.
+    (autograd flows through both copies).  Arithmetic follows xin's dtype, as the reference's
+    (deconv.py:49,61-67,104-106): fp32 inputs compute in fp32, fp64 inputs in fp64 (the generic
+    kernels' double instantiation, ADMM_TV_FLAG_F64), bf16/fp16 under ``torch.autocast`` compute in
+    fp32 and return fp32, as the reference does.
     """
     return _fft_admm_tv_impl(xin, lmbd, rho, kern, iso, maxit)
 
@@ -188,6 +189,7 @@ def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> 
         kern = torch.as_tensor(kern)
     _check_inputs(xin, kern)
     home, out_dtype = xin.device, (torch.float64 if xin.dtype == torch.float64 else torch.float32)
+    cdt = out_dtype  # the solve's arithmetic: fp64 for fp64 inputs, else fp32
     maxit = max(0, int(maxit))  # the reference loops over torch.arange(0, maxit): negative -> no iteration
     # empty batch: the reference's ops return an empty result of the same shape.  An empty shard of
     # an iso solve over ranks still runs: it must take part in every iteration's all-reduce.
@@ -204,17 +206,17 @@ def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> 
             from .._backward import fft_admm_tv_autograd
             out = fft_admm_tv_autograd(xin, lmbd, rho, kern, bool(iso), maxit, hook=hook)
         else:
-            x32 = xin.to(torch.float32).contiguous()  # differentiable cast (fp64 / autocast half inputs)
-            k32 = kern.to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \
-                torch.empty(0, dtype=torch.float32, device=dev)
+            xc = xin.to(cdt).contiguous()  # differentiable cast (autocast half inputs)
+            kc = kern.to(device=dev, dtype=cdt).contiguous() if kern.numel() > 0 else \
+                torch.empty(0, dtype=cdt, device=dev)
             psf_grad = kern.requires_grad and kern.numel() > 0
             out, _ = torch.ops.admm_hip.fft_admm_tv_fwd_train(
-                x32, _scalar_input(lmbd, dev), _scalar_input(rho, dev), k32, bool(iso), maxit, psf_grad)
+                xc, _scalar_input(lmbd, dev, cdt), _scalar_input(rho, dev, cdt), kc, bool(iso), maxit, psf_grad)
     else:
-        x32 = xin.detach().to(torch.float32).contiguous()
-        k32 = kern.detach().to(device=dev, dtype=torch.float32).contiguous() if kern.numel() > 0 else \
-            torch.empty(0, dtype=torch.float32, device=dev)
-        out = _solve(x32, k32, _as_device_scalar(lmbd, dev), _as_device_scalar(rho, dev), bool(iso), maxit,
+        xc = xin.detach().to(cdt).contiguous()
+        kc = kern.detach().to(device=dev, dtype=cdt).contiguous() if kern.numel() > 0 else \
+            torch.empty(0, dtype=cdt, device=dev)
+        out = _solve(xc, kc, _as_device_scalar(lmbd, dev, cdt), _as_device_scalar(rho, dev, cdt), bool(iso), maxit,
                      hook=hook)
     return out.to(device=home, dtype=out_dtype)
 

@@ -30,7 +30,7 @@ def shard_bounds(total: int, world: int, rank: int):
     return start, start + base + (1 if rank < rem else 0)
 
 
-def _as_tensor(v, device, dtype=torch.float32):
+def _as_tensor(v, device, dtype=torch.float64):
     if isinstance(v, torch.Tensor):
         return v.detach().reshape(-1)[:1].to(device=device, dtype=dtype).clone()
     return torch.tensor([float(v)], device=device, dtype=dtype)
@@ -49,14 +49,16 @@ def broadcast_params(kern: torch.Tensor, lmbd, rho, group=None, src: int = 0, de
     def trainable(v):
         return isinstance(v, torch.Tensor) and v.requires_grad
 
-    k = kern if trainable(kern) else (kern.detach().to(device=device, dtype=torch.float32).contiguous().clone()
+    # the PSF keeps its dtype (fp64 callers solve in fp64); lambda / rho travel as fp64 scalars
+    kdt = kern.dtype if (kern.numel() and kern.is_floating_point()) else torch.float32
+    k = kern if trainable(kern) else (kern.detach().to(device=device, dtype=kdt).contiguous().clone()
                                       if kern.numel() else torch.empty(0, device=device))
     lam = lmbd if trainable(lmbd) else _as_tensor(lmbd, device)
     rh = rho if trainable(rho) else _as_tensor(rho, device)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         parts = [t for t in (lam, rh, k) if not trainable(t)]
         if parts:
-            packed = torch.cat([t.reshape(-1) for t in parts])
+            packed = torch.cat([t.reshape(-1).to(torch.float64) for t in parts])  # one collective, exact
             dist.broadcast(packed, src=src, group=group)
             off = 0
             out = []
@@ -64,7 +66,7 @@ def broadcast_params(kern: torch.Tensor, lmbd, rho, group=None, src: int = 0, de
                 if trainable(t):
                     out.append(t)
                 else:
-                    out.append(packed[off:off + t.numel()].reshape(t.shape))
+                    out.append(packed[off:off + t.numel()].reshape(t.shape).to(t.dtype))
                     off += t.numel()
             lam, rh, k = out
     return k, lam, rh

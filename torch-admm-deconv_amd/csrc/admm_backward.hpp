@@ -63,6 +63,23 @@ __device__ __forceinline__ float shrink_vjp(float a, float zb, float tau, float 
 __device__ __forceinline__ float soft_dtau(float a, float zb, float tau) {
     return (fabsf(a) > tau) ? (a > 0.f ? -zb : zb) : 0.f;  // -sign(a) z^ on the active set
 }
+// fp64 (the generic kernels' double instantiation)
+template <bool ISO>
+__device__ __forceinline__ double shrink_vjp(double a, double zb, double tau, double n, double q) {
+    if constexpr (ISO) {
+        const double s = sqrt(n + 1e-15);
+        const double d = s + 1e-15;
+        const double f = 1.0 - tau / d;
+        if (!(f > 0.0)) return 0.0;
+        const double fp = tau / (d * d) * (0.5 / s);
+        return fma(f, zb, 2.0 * a * fp * q);
+    } else {
+        return (fabs(a) > tau) ? zb : 0.0;
+    }
+}
+__device__ __forceinline__ double soft_dtau(double a, double zb, double tau) {
+    return (fabs(a) > tau) ? (a > 0.0 ? -zb : zb) : 0.0;
+}
 
 // occupancy target of the reverse row pass (waves per SIMD), as PASSA_MINW for the forward:
 // 3 for aniso (measured -2.4 % at C3 size; a few registers spill), 2 for iso, whose extra
@@ -334,16 +351,16 @@ __global__ void __launch_bounds__(256) k_bwd_iso_q(BwdIsoArgs a) {
 
 // iso tau^: sum over pixels of -Q / (s + eps) where f > 0 (dz/dtau = -a / (s + eps));
 // one partial per block, fixed order.
-__global__ void k_iso_tau_partial(const float* __restrict__ q, const float* __restrict__ n,
-                                  const float* __restrict__ lam, const float* __restrict__ rho,
-                                  float* __restrict__ part, long long count) {
-    __shared__ float red[256];
-    const float tau = lam[0] / rho[0];
-    float acc = 0.f;
+template <class T = float>
+__global__ void k_iso_tau_partial(const T* __restrict__ q, const T* __restrict__ n, const T* __restrict__ lam,
+                                  const T* __restrict__ rho, T* __restrict__ part, long long count) {
+    __shared__ T red[256];
+    const T tau = lam[0] / rho[0];
+    T acc = 0;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count;
          i += (long long)gridDim.x * blockDim.x) {
-        const float s = sqrtf(n[i] + 1e-15f), d = s + 1e-15f;
-        if (1.f - tau / d > 0.f) acc += -q[i] / d;
+        const T s = sqrt(n[i] + eps15<T>()), d = s + eps15<T>();
+        if (T(1) - tau / d > T(0)) acc += -q[i] / d;
     }
     red[threadIdx.x] = acc;
     __syncthreads();
@@ -357,19 +374,20 @@ __global__ void k_iso_tau_partial(const float* __restrict__ q, const float* __re
 // final scalars of one module: tau^ = sum of its partials, rho^ = sum + tau^ * (-lam / rho^2),
 // lam^ = tau^ / rho.  part: [K][nstrips][2], the module's strips at [soff, soff + spm) of every
 // iteration; tpart (iso, or null): [K][G][ntp].  Single block, fixed order -> deterministic.
-__global__ void k_bwd_scalars(const float* __restrict__ part, int K, long long nstrips, long long spm, long long soff,
-                              const float* __restrict__ tpart, int ntp, int G, int g, const float* __restrict__ lam,
-                              const float* __restrict__ rho, float* __restrict__ glam, float* __restrict__ grho) {
+template <class T = float>
+__global__ void k_bwd_scalars(const T* __restrict__ part, int K, long long nstrips, long long spm, long long soff,
+                              const T* __restrict__ tpart, int ntp, int G, int g, const T* __restrict__ lam,
+                              const T* __restrict__ rho, T* __restrict__ glam, T* __restrict__ grho) {
     __shared__ double r1[256], r2[256];
     double sr = 0.0, st = 0.0;
     for (int it = 0; it < K; ++it) {
-        const float* pp = part + ((size_t)it * nstrips + soff) * 2;
+        const T* pp = part + ((size_t)it * nstrips + soff) * 2;
         for (long long i = threadIdx.x; i < spm; i += blockDim.x) {
             sr += pp[2 * i + 0];
             st += pp[2 * i + 1];
         }
         if (tpart) {
-            const float* tp = tpart + ((size_t)it * G + g) * ntp;
+            const T* tp = tpart + ((size_t)it * G + g) * ntp;
             for (int i = threadIdx.x; i < ntp; i += blockDim.x) st += tp[i];
         }
     }
@@ -386,8 +404,8 @@ __global__ void k_bwd_scalars(const float* __restrict__ part, int K, long long n
     if (threadIdx.x == 0) {
         const double l = lam[0], r = rho[0];
         const double tb = r2[0];
-        glam[0] = (float)(tb / r);
-        grho[0] = (float)(r1[0] - tb * l / (r * r));
+        glam[0] = (T)(tb / r);
+        grho[0] = (T)(r1[0] - tb * l / (r * r));
     }
 }
 
@@ -554,8 +572,9 @@ __global__ void k_xspec_reduce(const cf* __restrict__ part, int ngroups, long lo
 // Scalings: fast path -- row spectra carry a factor 2, fc is stored / (2HW):
 //   A_true = (HW)^2 A,  Z_true = Z / 4  (zscale 0.25);
 // generic path -- plain rfft spectra, fc stored / (HW): A_true = (HW)^2 A, Z_true = Z (zscale 1).
+template <class T = float>
 __global__ void k_psf_grad(const double2* __restrict__ A, const double2* __restrict__ Z,
-                           const double2* __restrict__ sigma, int k, int H, int W, float* __restrict__ gk,
+                           const double2* __restrict__ sigma, int k, int H, int W, T* __restrict__ gk,
                            double zscale) {
     __shared__ double red[256];
     const int tap = blockIdx.x;
@@ -590,7 +609,7 @@ __global__ void k_psf_grad(const double2* __restrict__ A, const double2* __restr
         if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
         __syncthreads();
     }
-    if (threadIdx.x == 0) gk[tap] = (float)red[0];
+    if (threadIdx.x == 0) gk[tap] = (T)red[0];
 }
 
 }  // namespace admm

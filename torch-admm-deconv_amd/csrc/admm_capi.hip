@@ -98,10 +98,15 @@ bool supported_hw(int64_t H, int64_t W) {
 // dimension fits their LDS image (two line buffers + twiddles and Bluestein tables, the latter read
 // from global memory for lines beyond ~6,800 points): up to 10,240
 constexpr int64_t kGenericMax = 10240;
-bool gen_fits(int n);  // below, with the plans
+bool gen_fits(int n, bool f64 = false);  // below, with the plans
 bool generic_hw(int64_t H, int64_t W) {
     return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax && gen_fits((int)H) &&
            gen_fits((int)W);
+}
+// fp64 solves (ADMM_TV_FLAG_F64) run on the generic kernels' double instantiation at every size
+bool is_f64(const admm_tv_desc& d) { return (d.flags & ADMM_TV_FLAG_F64) != 0; }
+bool f64_hw(int64_t H, int64_t W) {
+    return H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax && gen_fits((int)H, true) && gen_fits((int)W, true);
 }
 
 int env_int(const char* name, int dflt) {
@@ -109,7 +114,7 @@ int env_int(const char* name, int dflt) {
     return s ? std::atoi(s) : dflt;
 }
 
-GPlan make_plan(int n);  // generic-size transform plan (below)
+GPlan make_plan(int n, bool f64 = false);  // generic-size transform plan (below)
 
 // modules solved together (admm_tv_desc.groups)
 int ngroups_of(const admm_tv_desc& d) { return d.groups > 1 ? d.groups : 1; }
@@ -126,10 +131,12 @@ struct Layout {
 
 Layout make_layout(const admm_tv_desc& d) {
     Layout L{};
+    const bool f64 = is_f64(d);
+    const size_t rs = f64 ? sizeof(double) : sizeof(float), csz = 2 * rs;  // real / complex element
     const size_t G = ngroups_of(d);
     const size_t P = (size_t)d.B * d.C * G, H = d.H, W = d.W, N = W / 2;  // all modules' planes
-    const size_t img = P * H * W * sizeof(float);
-    const size_t img_m = (size_t)d.B * d.C * H * W * sizeof(float);         // one module's planes
+    const size_t img = P * H * W * rs;
+    const size_t img_m = (size_t)d.B * d.C * H * W * rs;         // one module's planes
     const int k = d.kh;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -137,8 +144,8 @@ Layout make_layout(const admm_tv_desc& d) {
         o += up(bytes);
         return at;
     };
-    L.gen = generic_hw(d.H, d.W);
-    L.spec[0] = take(L.gen ? P * H * (N + 1) * sizeof(cf) : img);
+    L.gen = f64 || generic_hw(d.H, d.W);
+    L.spec[0] = take(L.gen ? P * H * (N + 1) * csz : img);
     L.spec[1] = take(img);
     L.rimg = L.gen ? take(img) : 0;
     for (int i = 0; i < 4; ++i) L.u[i] = take(img);
@@ -147,11 +154,11 @@ Layout make_layout(const admm_tv_desc& d) {
     L.b = (k > 0 || !L.gen) ? take(img_m) : 0;
     // one Wiener factor per module (its rho); on the fused path followed by their packed copies for
     // the column pass (k_fc_pack)
-    L.fcT = take(G * (N + 1) * H * sizeof(float) * (L.gen ? 1 : 2));
-    L.mT = take((N + 1) * H * sizeof(cf));
+    L.fcT = take(G * (N + 1) * H * rs * (L.gen ? 1 : 2));
+    L.mT = take((N + 1) * H * csz);
     // twiddles; on the generic path followed by the plan's Bluestein tables (make_plan)
-    L.twW = take((W + (L.gen ? make_plan((int)W).ntab : 0)) * sizeof(cf));
-    L.twH = take((H + (L.gen ? make_plan((int)H).ntab : 0)) * sizeof(cf));
+    L.twW = take((W + (L.gen ? make_plan((int)W, f64).ntab : 0)) * csz);
+    L.twH = take((H + (L.gen ? make_plan((int)H, f64).ntab : 0)) * csz);
     L.twHd = take(H * sizeof(double2));
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
@@ -174,8 +181,8 @@ Layout make_layout(const admm_tv_desc& d) {
         }
         L.ppg = ppg;
         L.ngroups = (int)((P + ppg - 1) / ppg);
-        L.part = take((size_t)L.ngroups * 2 * H * W * sizeof(float));
-        L.nsq = take(G * 2 * H * W * sizeof(float));  // per module
+        L.part = take((size_t)L.ngroups * 2 * H * W * rs);
+        L.nsq = take(G * 2 * H * W * rs);  // per module
     }
     L.total = o;
     return L;
@@ -455,8 +462,9 @@ int validate(const admm_tv_desc* d) {
         d->kh < 0 || d->kw < 0 || d->groups < 0)
         return fail(ADMM_TV_EINVAL, "invalid sizes or maxit");
     if (d->kh != d->kw) return fail(ADMM_TV_ENONSQUARE, "non-square PSF (the reference's H_t swaps H/W pads)");
-    if (!supported_hw(d->H, d->W) && !generic_hw(d->H, d->W))
-        return fail(ADMM_TV_EUNSUPPORTED, "unsupported H, W (admm_tv_supported: generic sizes up to ~6,800)");
+    if (is_f64(*d) ? !f64_hw(d->H, d->W) : (!supported_hw(d->H, d->W) && !generic_hw(d->H, d->W)))
+        return fail(ADMM_TV_EUNSUPPORTED, "unsupported H, W (admm_tv_supported / admm_tv_supported_f64)");
+    if (is_f64(*d) && d->groups > 1) return fail(ADMM_TV_EUNSUPPORTED, "groups > 1: fp32 only");
     if (d->kh > d->H || d->kw > d->W) return fail(ADMM_TV_EKERNEL, "PSF larger than the image");
     if (d->groups > 1 && (!supported_hw(d->H, d->W) || (d->flags & ADMM_TV_FLAG_PSF_GRAD)))
         return fail(ADMM_TV_EUNSUPPORTED, "groups > 1 needs power-of-two H, W and no PSF gradient");
@@ -470,14 +478,16 @@ double spectra_scale(int H, int W) {
 }
 
 // setup: twiddle tables, PSF spectrum, Wiener factor (if rho given), centred-PSF multiplier
-int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, const float* rho, hipStream_t s) {
+template <class T>
+int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const T* kern, const T* rho, hipStream_t s) {
+    using C = cx_t<T>;
     ProfScope ps(3, s);
     const int H = (int)d.H, W = (int)d.W, N = W / 2, k = d.kh;
     const int nt = 256;
-    hipLaunchKernelGGL(k_tables, dim3((std::max(H, W) + nt - 1) / nt), dim3(nt), 0, s, at<cf>(ws, Lo.twW),
-                       at<cf>(ws, Lo.twH), at<double2>(ws, Lo.twHd), H, W);
+    hipLaunchKernelGGL(k_tables<C>, dim3((std::max(H, W) + nt - 1) / nt), dim3(nt), 0, s, at<C>(ws, Lo.twW),
+                       at<C>(ws, Lo.twH), at<double2>(ws, Lo.twHd), H, W);
     if (int e = launch_check("k_tables")) return e;
-    if (Lo.gen) {  // Bluestein tables of the row and column plans, after their twiddles
+    if (Lo.gen && !std::is_same<T, double>::value) {  // Bluestein tables of the row and column plans
         for (int dim = 0; dim < 2; ++dim) {
             const GPlan pl = make_plan(dim == 0 ? W : H);
             if (pl.ntab == 0) continue;
@@ -488,17 +498,18 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* kern, 
     }
     if (k > 0) {
         const int n = k * (N + 1);
-        hipLaunchKernelGGL(k_psf_rows, dim3((n + nt - 1) / nt), dim3(nt), 0, s, kern, at<double2>(ws, Lo.G), k, N, W);
+        hipLaunchKernelGGL(k_psf_rows<T>, dim3((n + nt - 1) / nt), dim3(nt), 0, s, kern, at<double2>(ws, Lo.G), k, N, W);
         if (int e = launch_check("k_psf_rows")) return e;
     }
     const int n = (N + 1) * H;
     if (rho) {
         for (int g = 0; g < ngroups_of(d); ++g) {  // one Wiener factor per module
-            hipLaunchKernelGGL(k_spectra, dim3((n + nt - 1) / nt), dim3(nt), 0, s, at<double2>(ws, Lo.G),
-                               at<double2>(ws, Lo.twHd), rho + g, at<float>(ws, Lo.fcT) + (size_t)g * n, at<cf>(ws, Lo.mT),
-                               k, H, N, W, Lo.sigma ? at<double2>(ws, Lo.sigma) : nullptr, spectra_scale(H, W));
+            hipLaunchKernelGGL(k_spectra<T>, dim3((n + nt - 1) / nt), dim3(nt), 0, s, at<double2>(ws, Lo.G),
+                               at<double2>(ws, Lo.twHd), rho + g, at<T>(ws, Lo.fcT) + (size_t)g * n, at<C>(ws, Lo.mT),
+                               k, H, N, W, Lo.sigma ? at<double2>(ws, Lo.sigma) : nullptr,
+                               (std::is_same<T, double>::value ? 1.0 / ((double)H * W) : spectra_scale(H, W)));
             if (int e = launch_check("k_spectra")) return e;
-            if (!Lo.gen) {
+            if constexpr (std::is_same<T, float>::value) if (!Lo.gen) {
                 float* fc = at<float>(ws, Lo.fcT) + (size_t)g * n;
                 hipLaunchKernelGGL(k_fc_pack, dim3((n + nt - 1) / nt), dim3(nt), 0, s, fc,
                                    fc + (size_t)ngroups_of(d) * n, H, N, col_e(H));
@@ -665,11 +676,42 @@ int blue_min() { return env_int("ADMM_BLUE_MIN", 41); }
 
 constexpr size_t kMaxLds = 160 * 1024;
 // LDS bytes of a generic transform kernel: twiddles + tables, two line buffers, Bluestein exchange
-size_t glds(int n, int lines, const GPlan& p) {
-    return sizeof(cf) * ((p.twg ? 0 : (size_t)n + p.ntab) + 2 * (size_t)n * lines + p.xslots);
+// (csz: bytes of a complex element, 16 for the fp64 kernels)
+size_t glds(int n, int lines, const GPlan& p, size_t csz = sizeof(cf)) {
+    return csz * ((p.twg ? 0 : (size_t)n + p.ntab) + 2 * (size_t)n * lines + p.xslots);
 }
 
-GPlan make_plan(int n) {
+// fp64 plan: any prime > 5 first (its stage at NS = 1 needs no twiddle pass), then radices 4, 2, 3, 5
+// (the radices the double kernels have butterflies for; no Bluestein stages); twiddles from global
+// memory when a line's LDS image would not fit
+GPlan make_plan_f64(int n) {
+    GPlan p{};
+    p.n = n;
+    int m = n, r = n;
+    auto take_all = [&](int q) {
+        while (m % q == 0 && m > 1) {
+            p.rad[p.nst++] = q;
+            m /= q;
+        }
+    };
+    for (int q : {2, 3, 5})
+        while (r % q == 0) r /= q;
+    for (int f = 7; f * f <= r; f += 2)
+        if (r % f == 0) {
+            take_all(f);
+            while (r % f == 0) r /= f;
+        }
+    if (r > 1) take_all(r);
+    take_all(4);
+    take_all(2);
+    take_all(3);
+    take_all(5);
+    p.twg = glds(n, 1, p, sizeof(double2)) > kMaxLds ? 1 : 0;
+    return p;
+}
+
+GPlan make_plan(int n, bool f64) {
+    if (f64) return make_plan_f64(n);
     GPlan p = make_plan_radices(n);
     const int bmin = blue_min();
     int M = 0;  // one Bluestein size for the plan: M = 2^k >= 2R - 1 for its largest such prime
@@ -698,7 +740,9 @@ GPlan make_plan(int n) {
     return q;
 }
 
-bool gen_fits(int n) { return glds(n, 1, make_plan(n)) <= kMaxLds; }
+bool gen_fits(int n, bool f64) {
+    return glds(n, 1, make_plan(n, f64), f64 ? sizeof(double2) : sizeof(cf)) <= kMaxLds;
+}
 
 // threads per block of the generic transform kernels (A/B knob; 64, 128 or 256)
 int gen_threads(const char* knob) {
@@ -797,15 +841,17 @@ int pow2_floor(int v) { int p = 1; while (2 * p <= v) p *= 2; return p; }
 // With Bluestein stages the column pass takes at least as many columns as make one item per
 // sub-group (16x3x509^2: 2 -> 4 columns, 1,125 -> 1,368 it/s; BSD keeps 4).  Either count is
 // halved until the block's LDS fits.
-int fit_lines(int n, int lines, const GPlan& p) {
-    while (lines > 1 && glds(n, lines, p) > kMaxLds) lines /= 2;
+int fit_lines(int n, int lines, const GPlan& p, size_t csz = sizeof(cf)) {
+    while (lines > 1 && glds(n, lines, p, csz) > kMaxLds) lines /= 2;
     return lines;
 }
-int grow_lines(int W, const GPlan& p) {
+int grow_lines(int W, const GPlan& p, size_t csz = sizeof(cf)) {
+    if (csz != sizeof(cf)) return fit_lines(W, pow2_floor(std::max(1, std::min(32, (2048 / W - 1) / 2))), p, csz);
     const int dflt = pow2_floor(std::max(1, std::min(32, (4096 / W - 1) / 2)));
     return fit_lines(W, pow2_floor(std::max(1, std::min(32, env_int("ADMM_GROW_LINES", dflt)))), p);
 }
-int gcol_cols(int H, const GPlan& p) {
+int gcol_cols(int H, const GPlan& p, size_t csz = sizeof(cf)) {
+    if (csz != sizeof(cf)) return fit_lines(H, pow2_floor(std::max(1, std::min(16, (3072 / H - 1) / 2))), p, csz);
     // column blocks: ~48 KB LDS images without Bluestein stages (VGA 480: 2 -> 4 columns +7 %,
     // 500: +4 %, HD 1080: 1 -> 2 columns +6 %; tools/bench_generic_sizes.py), ~32 KB with them
     int dflt = pow2_floor(std::max(1, std::min(16, ((p.bm > 0 ? 4096 : 6144) / H - 1) / 2)));
@@ -819,96 +865,122 @@ int gcol_cols(int H, const GPlan& p) {
     return fit_lines(H, pow2_floor(std::max(1, std::min(32, env_int("ADMM_GCOL_COLS", dflt)))), p);
 }
 
-int grow_fwd(const float* img, cf* spec, const cf* tw, int W, long long rows, hipStream_t s) {
-    const GPlan pl = make_plan(W);
-    GRowArgs a{img, spec, nullptr, tw, pl, rows, grow_lines(W, pl)};
-    const size_t lds = glds(W, a.lines, a.plan);
-    return with_plan(a.plan, [&](auto bm, auto twg) {
+// the launchers below are templated on the real type T of the solve: float, or double for fp64
+// inputs (ADMM_TV_FLAG_F64: the generic kernels' double instantiation, plans without Bluestein
+// stages, 256-thread blocks)
+template <class T> constexpr bool kF64 = std::is_same<T, double>::value;
+template <class T> constexpr size_t kCsz = sizeof(cx_t<T>);
+
+// f(integral_constant BM, bool_constant TWG) for a plan: the fp64 kernels exist for BM = 0 only
+template <class T, class F> int with_plan_t(const GPlan& p, F&& f) {
+    if constexpr (kF64<T>) {
+        if (p.bm != 0) return fail(ADMM_TV_EUNSUPPORTED, "fp64 plan with a Bluestein stage");
+        if (p.twg) return f(std::integral_constant<int, 0>{}, std::true_type{});
+        return f(std::integral_constant<int, 0>{}, std::false_type{});
+    } else {
+        return with_plan(p, f);
+    }
+}
+
+template <class T>
+int grow_fwd(const T* img, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, hipStream_t s) {
+    const GPlan pl = make_plan(W, kF64<T>);
+    GRowArgsT<T> a{img, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>)};
+    const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
+    return with_plan_t<T>(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
         const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
-        if constexpr (BM == 0) {
+        if constexpr (BM == 0 && !kF64<T>) {
             if (gen_wide(W, pl)) {
                 if (int e = set_lds(k_grow_fwd<BM, TWG, kGenWide>, lds)) return e;
                 hipLaunchKernelGGL((k_grow_fwd<BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
                 return launch_check("k_grow_fwd");
             }
         }
-        if (int e = set_lds(k_grow_fwd<BM, TWG>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_fwd<BM, TWG>), grid, dim3(gen_threads("ADMM_GROW_NT")), lds, s, a);
+        if (int e = set_lds(k_grow_fwd<BM, TWG, GNT, T>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_fwd<BM, TWG, GNT, T>), grid, dim3(kF64<T> ? GNT : gen_threads("ADMM_GROW_NT")), lds,
+                           s, a);
         return launch_check("k_grow_fwd");
     });
 }
 // the step fused into the row transform of r (k_grow_fwd_step; inference iterations)
-template <bool ISO, bool FIRST>
-int grow_fwd_step_t(const GStepArgs& g, cf* spec, const cf* tw, int W, long long rows, hipStream_t s) {
-    const GPlan pl = make_plan(W);
-    GRowArgs a{nullptr, spec, nullptr, tw, pl, rows, grow_lines(W, pl)};
-    const size_t lds = glds(W, a.lines, a.plan);
-    return with_plan(a.plan, [&](auto bm, auto twg) {
+template <bool ISO, bool FIRST, class T>
+int grow_fwd_step_t(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, hipStream_t s) {
+    const GPlan pl = make_plan(W, kF64<T>);
+    GRowArgsT<T> a{nullptr, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>)};
+    const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
+    return with_plan_t<T>(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
         const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
-        if constexpr (BM == 0) {
+        if constexpr (BM == 0 && !kF64<T>) {
             if (gen_wide(W, pl)) {
                 if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST, kGenWide>, lds)) return e;
                 hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST, kGenWide>), grid, dim3(kGenWide), lds, s, a, g);
                 return launch_check("k_grow_fwd_step");
             }
         }
-        if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST>), grid, dim3(gen_threads("ADMM_GROW_NT")), lds, s, a, g);
+        if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST, GNT, T>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST, GNT, T>), grid,
+                           dim3(kF64<T> ? GNT : gen_threads("ADMM_GROW_NT")), lds, s, a, g);
         return launch_check("k_grow_fwd_step");
     });
 }
-int grow_fwd_step(const GStepArgs& g, cf* spec, const cf* tw, int W, long long rows, bool iso, bool first,
-                  hipStream_t s) {
+template <class T>
+int grow_fwd_step(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, bool iso,
+                  bool first, hipStream_t s) {
     if (iso) return first ? grow_fwd_step_t<true, true>(g, spec, tw, W, rows, s)
                           : grow_fwd_step_t<true, false>(g, spec, tw, W, rows, s);
     return first ? grow_fwd_step_t<false, true>(g, spec, tw, W, rows, s)
                  : grow_fwd_step_t<false, false>(g, spec, tw, W, rows, s);
 }
-int grow_inv(const cf* spec, float* img, const cf* tw, int W, long long rows, hipStream_t s) {
-    const GPlan pl = make_plan(W);
-    GRowArgs a{nullptr, const_cast<cf*>(spec), img, tw, pl, rows, grow_lines(W, pl)};
-    const size_t lds = glds(W, a.lines, a.plan);
-    return with_plan(a.plan, [&](auto bm, auto twg) {
+template <class T>
+int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long rows, hipStream_t s) {
+    const GPlan pl = make_plan(W, kF64<T>);
+    GRowArgsT<T> a{nullptr, const_cast<cx_t<T>*>(spec), img, tw, pl, rows, grow_lines(W, pl, kCsz<T>)};
+    const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
+    return with_plan_t<T>(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
         const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
-        if constexpr (BM == 0) {
+        if constexpr (BM == 0 && !kF64<T>) {
             if (gen_wide(W, pl)) {
                 if (int e = set_lds(k_grow_inv<BM, TWG, kGenWide>, lds)) return e;
                 hipLaunchKernelGGL((k_grow_inv<BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
                 return launch_check("k_grow_inv");
             }
         }
-        if (int e = set_lds(k_grow_inv<BM, TWG>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_inv<BM, TWG>), grid, dim3(gen_threads("ADMM_GROW_NT")), lds, s, a);
+        if (int e = set_lds(k_grow_inv<BM, TWG, GNT, T>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_inv<BM, TWG, GNT, T>), grid, dim3(kF64<T> ? GNT : gen_threads("ADMM_GROW_NT")), lds,
+                           s, a);
         return launch_check("k_grow_inv");
     });
 }
-template <int MODE, int BM, bool TWG> int gcol_launch(const GColArgs& a, size_t lds, dim3 grid, hipStream_t s) {
-    if constexpr (BM == 0) {
+template <int MODE, int BM, bool TWG, class T>
+int gcol_launch(const GColArgsT<T>& a, size_t lds, dim3 grid, hipStream_t s) {
+    if constexpr (BM == 0 && !kF64<T>) {
         if (gen_wide(a.plan.n, a.plan)) {
             if (int e = set_lds(k_gcol<MODE, BM, TWG, kGenWide>, lds)) return e;
             hipLaunchKernelGGL((k_gcol<MODE, BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
             return launch_check("k_gcol");
         }
     }
-    if (int e = set_lds(k_gcol<MODE, BM, TWG>, lds)) return e;
-    hipLaunchKernelGGL((k_gcol<MODE, BM, TWG>), grid, dim3(gen_threads("ADMM_GCOL_NT")), lds, s, a);
+    if (int e = set_lds(k_gcol<MODE, BM, TWG, GNT, T>, lds)) return e;
+    hipLaunchKernelGGL((k_gcol<MODE, BM, TWG, GNT, T>), grid, dim3(kF64<T> ? GNT : gen_threads("ADMM_GCOL_NT")), lds,
+                       s, a);
     return launch_check("k_gcol");
 }
-int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H, int W, long long P, int mode,
-         hipStream_t s) {
-    const GPlan pl = make_plan(H);
-    const int Wh = W / 2 + 1, cols = gcol_cols(H, pl);
+template <class T>
+int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx_t<T>* tw, int H, int W, long long P,
+         int mode, hipStream_t s) {
+    const GPlan pl = make_plan(H, kF64<T>);
+    const int Wh = W / 2 + 1, cols = gcol_cols(H, pl, kCsz<T>);
     const int colblocks = (Wh + cols - 1) / cols;
-    GColArgs a{spec, dump, fcT, mT, tw, pl, Wh, cols, colblocks, P};
-    const size_t lds = glds(H, cols, a.plan);
+    GColArgsT<T> a{spec, dump, fcT, mT, tw, pl, Wh, cols, colblocks, P};
+    const size_t lds = glds(H, cols, a.plan, kCsz<T>);
     const dim3 grid((unsigned)(P * colblocks));
-    return with_plan(a.plan, [&](auto bm, auto twg) {
+    return with_plan_t<T>(a.plan, [&](auto bm, auto twg) {
         constexpr int BM = decltype(bm)::value;
         constexpr bool TWG = decltype(twg)::value;
         switch (mode) {
@@ -920,18 +992,20 @@ int gcol(cf* spec, cf* dump, const float* fcT, const cf* mT, const cf* tw, int H
     });
 }
 // img_out = real part of the 2-D transform chain  rowFFT -> column pass (mode) -> rowIFFT  of img_in
-int gapply(const float* img_in, float* img_out, cf* spec, const Layout& Lo, void* ws, const admm_tv_desc& d, int mode,
+template <class T>
+int gapply(const T* img_in, T* img_out, cx_t<T>* spec, const Layout& Lo, void* ws, const admm_tv_desc& d, int mode,
            hipStream_t s) {
+    using C = cx_t<T>;
     const long long P = d.B * d.C, rows = P * d.H;
     const int H = (int)d.H, W = (int)d.W;
-    cf* twW = at<cf>(ws, Lo.twW);
+    C* twW = at<C>(ws, Lo.twW);
     if (int e = grow_fwd(img_in, spec, twW, W, rows, s)) return e;
-    if (int e = gcol(spec, nullptr, at<float>(ws, Lo.fcT), at<cf>(ws, Lo.mT), at<cf>(ws, Lo.twH), H, W, P, mode, s))
+    if (int e = gcol<T>(spec, nullptr, at<T>(ws, Lo.fcT), at<C>(ws, Lo.mT), at<C>(ws, Lo.twH), H, W, P, mode, s))
         return e;
-    return grow_inv(spec, img_out, twW, W, rows, s);
+    return grow_inv<T>(spec, img_out, twW, W, rows, s);
 }
 
-int gstep(const GStepArgs& a, bool iso, bool first, bool hist, hipStream_t s) {
+template <class T> int gstep(const GStepArgsT<T>& a, bool iso, bool first, bool hist, hipStream_t s) {
     // one block row per image row (P H <= 2^31 - 1 rows), column chunks of 256 pixels
     const long long rows = a.npx / a.W;
     if (rows <= 0) return 0;
@@ -939,30 +1013,30 @@ int gstep(const GStepArgs& a, bool iso, bool first, bool hist, hipStream_t s) {
     const dim3 grid((unsigned)rows, (unsigned)((a.W + 255) / 256)), blk(256);
     const int sel = (iso ? 4 : 0) | (first ? 2 : 0) | (hist ? 1 : 0);
     switch (sel) {
-        case 0: hipLaunchKernelGGL((k_gstep<false, false, false>), grid, blk, 0, s, a); break;
-        case 1: hipLaunchKernelGGL((k_gstep<false, false, true>), grid, blk, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_gstep<false, true, false>), grid, blk, 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_gstep<false, true, true>), grid, blk, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_gstep<true, false, false>), grid, blk, 0, s, a); break;
-        case 5: hipLaunchKernelGGL((k_gstep<true, false, true>), grid, blk, 0, s, a); break;
-        case 6: hipLaunchKernelGGL((k_gstep<true, true, false>), grid, blk, 0, s, a); break;
-        default: hipLaunchKernelGGL((k_gstep<true, true, true>), grid, blk, 0, s, a); break;
+        case 0: hipLaunchKernelGGL((k_gstep<false, false, false, T>), grid, blk, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_gstep<false, false, true, T>), grid, blk, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_gstep<false, true, false, T>), grid, blk, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_gstep<false, true, true, T>), grid, blk, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_gstep<true, false, false, T>), grid, blk, 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_gstep<true, false, true, T>), grid, blk, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_gstep<true, true, false, T>), grid, blk, 0, s, a); break;
+        default: hipLaunchKernelGGL((k_gstep<true, true, true, T>), grid, blk, 0, s, a); break;
     }
     return launch_check("k_gstep");
 }
 
-int gbwd(const GBwdArgs& a, bool iso, bool lastk, bool firstk, hipStream_t s) {
+template <class T> int gbwd(const GBwdArgsT<T>& a, bool iso, bool lastk, bool firstk, hipStream_t s) {
     const dim3 grid((unsigned)((a.npx + 255) / 256)), blk(256);
     const int sel = (iso ? 4 : 0) | (lastk ? 2 : 0) | (firstk ? 1 : 0);
     switch (sel) {
-        case 0: hipLaunchKernelGGL((k_gbwd<false, false, false>), grid, blk, 0, s, a); break;
-        case 1: hipLaunchKernelGGL((k_gbwd<false, false, true>), grid, blk, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_gbwd<false, true, false>), grid, blk, 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_gbwd<false, true, true>), grid, blk, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_gbwd<true, false, false>), grid, blk, 0, s, a); break;
-        case 5: hipLaunchKernelGGL((k_gbwd<true, false, true>), grid, blk, 0, s, a); break;
-        case 6: hipLaunchKernelGGL((k_gbwd<true, true, false>), grid, blk, 0, s, a); break;
-        default: hipLaunchKernelGGL((k_gbwd<true, true, true>), grid, blk, 0, s, a); break;
+        case 0: hipLaunchKernelGGL((k_gbwd<false, false, false, T>), grid, blk, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_gbwd<false, false, true, T>), grid, blk, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_gbwd<false, true, false, T>), grid, blk, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_gbwd<false, true, true, T>), grid, blk, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_gbwd<true, false, false, T>), grid, blk, 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_gbwd<true, false, true, T>), grid, blk, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_gbwd<true, true, false, T>), grid, blk, 0, s, a); break;
+        default: hipLaunchKernelGGL((k_gbwd<true, true, true, T>), grid, blk, 0, s, a); break;
     }
     return launch_check("k_gbwd");
 }
@@ -979,48 +1053,51 @@ struct Hist {
 };
 Hist make_hist(const admm_tv_desc& d) {
     Hist h{};
+    const size_t rs = is_f64(d) ? sizeof(double) : sizeof(float);
     const size_t G = ngroups_of(d);
-    const size_t img = G * d.B * d.C * d.H * d.W * sizeof(float);
+    const size_t img = G * d.B * d.C * d.H * d.W * rs;
     h.a_slot = up(img);
-    h.n_slot = d.iso ? up(G * 2 * (size_t)d.H * d.W * sizeof(float)) : 0;
+    h.n_slot = d.iso ? up(G * 2 * (size_t)d.H * d.W * rs) : 0;
     h.n_off = (size_t)d.maxit * 2 * h.a_slot;
     h.t_off = h.n_off + (size_t)d.maxit * h.n_slot;
     h.keep_t = d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD);
-    h.t_slot = generic_hw(d.H, d.W) ? up((size_t)d.B * d.C * d.H * (d.W / 2 + 1) * sizeof(cf)) : h.a_slot;
+    h.t_slot = (is_f64(d) || generic_hw(d.H, d.W)) ? up((size_t)d.B * d.C * d.H * (d.W / 2 + 1) * 2 * rs) : h.a_slot;
     h.total = h.t_off + (h.keep_t ? (size_t)d.maxit * h.t_slot : 0);
     return h;
 }
 
 
 // generic-size forward (same contract as run_forward; generic_kernels.hpp)
-int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, const float* lam, const float* rho,
-                    float* out, void* ws, void* hist, hipStream_t s) {
+template <class T>
+int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const T* lam, const T* rho, T* out, void* ws,
+                    void* hist, hipStream_t s) {
+    using C = cx_t<T>;
     const long long P = d.B * d.C;
     const int H = (int)d.H, W = (int)d.W;
-    cf* twW = at<cf>(ws, Lo.twW);
-    cf* twH = at<cf>(ws, Lo.twH);
-    float* fcT = at<float>(ws, Lo.fcT);
-    cf* mT = at<cf>(ws, Lo.mT);
-    cf* spec = at<cf>(ws, Lo.spec[0]);
-    float* ximg = at<float>(ws, Lo.spec[1]);
-    float* rimg = at<float>(ws, Lo.rimg);
-    float* u[4] = {at<float>(ws, Lo.u[0]), at<float>(ws, Lo.u[1]), at<float>(ws, Lo.u[2]), at<float>(ws, Lo.u[3])};
+    C* twW = at<C>(ws, Lo.twW);
+    C* twH = at<C>(ws, Lo.twH);
+    T* fcT = at<T>(ws, Lo.fcT);
+    C* mT = at<C>(ws, Lo.mT);
+    C* spec = at<C>(ws, Lo.spec[0]);
+    T* ximg = at<T>(ws, Lo.spec[1]);
+    T* rimg = at<T>(ws, Lo.rimg);
+    T* u[4] = {at<T>(ws, Lo.u[0]), at<T>(ws, Lo.u[1]), at<T>(ws, Lo.u[2]), at<T>(ws, Lo.u[3])};
     const bool train = hist != nullptr;
     const Hist Hs = make_hist(d);
-    auto ha = [&](int k, int comp) -> float* {
-        return reinterpret_cast<float*>(static_cast<char*>(hist) + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
+    auto ha = [&](int k, int comp) -> T* {
+        return reinterpret_cast<T*>(static_cast<char*>(hist) + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
     };
-    auto hn = [&](int k) -> float* {
-        return reinterpret_cast<float*>(static_cast<char*>(hist) + Hs.n_off + (size_t)(k - 1) * Hs.n_slot);
+    auto hn = [&](int k) -> T* {
+        return reinterpret_cast<T*>(static_cast<char*>(hist) + Hs.n_off + (size_t)(k - 1) * Hs.n_slot);
     };
     const bool keep_t = train && Hs.keep_t;  // PSF gradient: keep every r_k's 2-D spectrum
-    auto ht = [&](int k) -> cf* {
-        return reinterpret_cast<cf*>(static_cast<char*>(hist) + Hs.t_off + (size_t)(k - 1) * Hs.t_slot);
+    auto ht = [&](int k) -> C* {
+        return reinterpret_cast<C*>(static_cast<char*>(hist) + Hs.t_off + (size_t)(k - 1) * Hs.t_slot);
     };
-    const float* bimg = xin;
+    const T* bimg = xin;
     if (d.kh > 0) {  // b = H_t(xin) once
         ProfScope ps(3, s);
-        float* bb = at<float>(ws, Lo.b);
+        T* bb = at<T>(ws, Lo.b);
         if (int e = gapply(xin, bb, spec, Lo, ws, d, 1, s)) return e;
         bimg = bb;
     }
@@ -1028,11 +1105,11 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, c
     // whose planes are independent -- one half per stream, ADMM_GEN_STREAMS)
     auto solve_planes = [&](long long p0, long long np, hipStream_t st) -> int {
     const size_t so = (size_t)p0 * H * (W / 2 + 1), io = (size_t)p0 * H * W;  // cf / float offsets
-    cf* cspec = spec + so;
-    float* cx = ximg + io;
-    float* crimg = rimg + io;
-    float* cout = out + io;
-    const float* cb = bimg + io;
+    C* cspec = spec + so;
+    T* cx = ximg + io;
+    T* crimg = rimg + io;
+    T* cout = out + io;
+    const T* cb = bimg + io;
     const long long crows = np * H;
     {
         ProfScope ps(3, st);
@@ -1043,14 +1120,14 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, c
         const bool last = it == d.maxit;
         {
             ProfScope ps(1, st);
-            if (int e = gcol(cspec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, np, 0, st)) return e;
-            if (int e = grow_inv(cspec, last ? cout : cx, twW, W, crows, st)) return e;
+            if (int e = gcol<T>(cspec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, np, 0, st)) return e;
+            if (int e = grow_inv<T>(cspec, last ? cout : cx, twW, W, crows, st)) return e;
         }
         if (last && !train) break;
-        const float* xk = last ? cout : cx;
+        const T* xk = last ? cout : cx;
         const bool first = it == 1;
-        const float *uxi, *uyi, *nprev = nullptr;
-        float *uxo, *uyo;
+        const T *uxi, *uyi, *nprev = nullptr;
+        T *uxo, *uyo;
         if (train) {
             uxi = first ? nullptr : ha(it - 1, 0);
             uyi = first ? nullptr : ha(it - 1, 1);
@@ -1063,25 +1140,25 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const float* xin, c
             uxo = u[2 * (1 - uin)] + io;
             uyo = u[2 * (1 - uin) + 1] + io;
         }
-        const float* nsq = nullptr;
+        const T* nsq = nullptr;
         if (d.iso) {
             ProfScope ps(2, st);
-            float* nout = train ? hn(it) : at<float>(ws, Lo.nsq);
+            T* nout = train ? hn(it) : at<T>(ws, Lo.nsq);
             const long long hw = (long long)H * W;
             const dim3 grid((unsigned)((hw + 255) / 256)), blk(256);
             if (first)
-                hipLaunchKernelGGL((k_giso_norm<true, false>), grid, blk, 0, st, xk, uxi, uyi, nprev, lam, rho, nout, H, W, np);
+                hipLaunchKernelGGL((k_giso_norm<true, false, T>), grid, blk, 0, st, xk, uxi, uyi, nprev, lam, rho, nout, H, W, np);
             else if (train)
-                hipLaunchKernelGGL((k_giso_norm<false, true>), grid, blk, 0, st, xk, uxi, uyi, nprev, lam, rho, nout, H, W, np);
+                hipLaunchKernelGGL((k_giso_norm<false, true, T>), grid, blk, 0, st, xk, uxi, uyi, nprev, lam, rho, nout, H, W, np);
             else
-                hipLaunchKernelGGL((k_giso_norm<false, false>), grid, blk, 0, st, xk, uxi, uyi, nprev, lam, rho, nout, H, W, np);
+                hipLaunchKernelGGL((k_giso_norm<false, false, T>), grid, blk, 0, st, xk, uxi, uyi, nprev, lam, rho, nout, H, W, np);
             if (int e = launch_check("k_giso_norm")) return e;
-            allreduce(d, nout, 2ull * H * W, st);
+            allreduce(d, reinterpret_cast<float*>(nout), 2ull * H * W, st);
             nsq = nout;
         }
         {
             ProfScope ps(0, st);
-            GStepArgs ga{xk, cb, uxi, uyi, uxo, uyo, last ? nullptr : crimg, nsq, nprev, lam, rho, H, W, np * H * W};
+            GStepArgsT<T> ga{xk, cb, uxi, uyi, uxo, uyo, last ? nullptr : crimg, nsq, nprev, lam, rho, H, W, np * H * W};
             // inference: the step runs inside the row transform of r (ADMM_GSTEP_FUSE=0: separate)
             if (!train && !last && env_int("ADMM_GSTEP_FUSE", 1)) {
                 if (int e = grow_fwd_step(ga, cspec, twW, W, crows, d.iso != 0, first, st)) return e;
@@ -1297,8 +1374,9 @@ struct BwdLayout {
 BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     BwdLayout B{};
     B.f = make_layout(d);
+    const size_t rs = is_f64(d) ? sizeof(double) : sizeof(float);
     const size_t G = ngroups_of(d);
-    const size_t img = G * d.B * d.C * d.H * d.W * sizeof(float);  // all modules' planes
+    const size_t img = G * d.B * d.C * d.H * d.W * rs;  // all modules' planes
     size_t o = B.f.total;
     auto take = [&](size_t bytes) {
         size_t at_ = o;
@@ -1315,16 +1393,16 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
         B.R = strip_rows((int)d.H, (int)d.W / 2, rows);
         B.nstrips = rows / B.R;
     }
-    B.part = take((size_t)std::max(d.maxit, 1) * B.nstrips * 2 * sizeof(float));
+    B.part = take((size_t)std::max(d.maxit, 1) * B.nstrips * 2 * rs);
     B.ntp = 256;
-    B.tpart = take((size_t)std::max(d.maxit, 1) * G * B.ntp * sizeof(float));  // [K][G][ntp]
-    B.q = take(G * 2 * (size_t)d.H * d.W * sizeof(float));
+    B.tpart = take((size_t)std::max(d.maxit, 1) * G * B.ntp * rs);  // [K][G][ntp]
+    B.q = take(G * 2 * (size_t)d.H * d.W * rs);
     if (d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) {
         const size_t nf = ((size_t)d.W / 2 + 1) * d.H;
         B.xppg = 8;
         B.xgroups = (int)((d.B * d.C + B.xppg - 1) / B.xppg);
         // fast path: per-plane-group cross-spectrum partials; generic: one 2-D spectrum set
-        B.xpart = take((B.f.gen ? (size_t)d.B * d.C : (size_t)B.xgroups) * nf * sizeof(cf));
+        B.xpart = take((B.f.gen ? (size_t)d.B * d.C : (size_t)B.xgroups) * nf * 2 * rs);
         B.aacc = take(nf * sizeof(double2));
         B.zacc = take(nf * sizeof(double2));
     }
@@ -1334,9 +1412,10 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
 
 
 // generic-size backward (same contract as admm_tv_backward, PSF gradient excluded)
-int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xin, const float* lam, const float* rho,
-                     const float* gout, const void* hist, float* gxin, float* glam, float* grho, float* gkern, void* ws,
-                     hipStream_t s) {
+template <class T>
+int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, const T* lam, const T* rho,
+                     const T* gout, const void* hist, T* gxin, T* glam, T* grho, T* gkern, void* ws, hipStream_t s) {
+    using C = cx_t<T>;
     const Layout& Lo = BL.f;
     const long long P = d.B * d.C;
     const int H = (int)d.H, W = (int)d.W, K = d.maxit;
@@ -1344,35 +1423,35 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xi
     const long long HW = (long long)H * W;
     const Hist Hs = make_hist(d);
     char* hb = static_cast<char*>(const_cast<void*>(hist));
-    auto ha = [&](int k, int comp) -> const float* {
-        return reinterpret_cast<const float*>(hb + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
+    auto ha = [&](int k, int comp) -> const T* {
+        return reinterpret_cast<const T*>(hb + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
     };
-    auto hn = [&](int k) -> const float* { return reinterpret_cast<const float*>(hb + Hs.n_off + (size_t)(k - 1) * Hs.n_slot); };
-    auto ht = [&](int k) -> const cf* { return reinterpret_cast<const cf*>(hb + Hs.t_off + (size_t)(k - 1) * Hs.t_slot); };
+    auto hn = [&](int k) -> const T* { return reinterpret_cast<const T*>(hb + Hs.n_off + (size_t)(k - 1) * Hs.n_slot); };
+    auto ht = [&](int k) -> const C* { return reinterpret_cast<const C*>(hb + Hs.t_off + (size_t)(k - 1) * Hs.t_slot); };
     const bool psf_grad = gkern != nullptr;
     const int Wh = W / 2 + 1;
     const long long nf = (long long)Wh * H;
-    cf* xspec = psf_grad ? at<cf>(ws, BL.xpart) : nullptr;  // 2-D spectra of x^_k (then of b^)
+    C* xspec = psf_grad ? at<C>(ws, BL.xpart) : nullptr;  // 2-D spectra of x^_k (then of b^)
     if (psf_grad) {
         HIPCHK(hipMemsetAsync(at<double2>(ws, BL.aacc), 0, nf * sizeof(double2), s));
         HIPCHK(hipMemsetAsync(at<double2>(ws, BL.zacc), 0, nf * sizeof(double2), s));
     }
-    cf* twW = at<cf>(ws, Lo.twW);
-    cf* twH = at<cf>(ws, Lo.twH);
-    float* fcT = at<float>(ws, Lo.fcT);
+    C* twW = at<C>(ws, Lo.twW);
+    C* twH = at<C>(ws, Lo.twH);
+    T* fcT = at<T>(ws, Lo.fcT);
     const long long rows = P * H;
     const dim3 fgrid((unsigned)((nf + 255) / 256)), fblk(256);
-    cf* spec = at<cf>(ws, Lo.spec[0]);
-    float* rb = at<float>(ws, Lo.spec[1]);   // r^_k
-    float* xbuf[2] = {at<float>(ws, Lo.rimg), at<float>(ws, Lo.u[0])};  // x^ ping-pong
-    float* ab[4] = {at<float>(ws, BL.abar[0]), at<float>(ws, BL.abar[1]), at<float>(ws, BL.abar[2]),
-                    at<float>(ws, BL.abar[3])};
-    float* bbar = (d.kh == 0 && gxin) ? gxin : at<float>(ws, BL.bbar);
-    float* part = at<float>(ws, BL.part);
-    float* tpart = at<float>(ws, BL.tpart);
-    float* q = at<float>(ws, BL.q);
-    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * BL.ntp * sizeof(float), s));
-    const float* xbk = gout;
+    C* spec = at<C>(ws, Lo.spec[0]);
+    T* rb = at<T>(ws, Lo.spec[1]);   // r^_k
+    T* xbuf[2] = {at<T>(ws, Lo.rimg), at<T>(ws, Lo.u[0])};  // x^ ping-pong
+    T* ab[4] = {at<T>(ws, BL.abar[0]), at<T>(ws, BL.abar[1]), at<T>(ws, BL.abar[2]),
+                    at<T>(ws, BL.abar[3])};
+    T* bbar = (d.kh == 0 && gxin) ? gxin : at<T>(ws, BL.bbar);
+    T* part = at<T>(ws, BL.part);
+    T* tpart = at<T>(ws, BL.tpart);
+    T* q = at<T>(ws, BL.q);
+    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * BL.ntp * sizeof(T), s));
+    const T* xbk = gout;
     int ain = 0, xo = 0;
     for (int k = K; k >= 1; --k) {
         const bool lastk = (k == K), firstk = (k == 1);
@@ -1381,10 +1460,10 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xi
             // r^_k = M x^_k; with the PSF gradient the column pass also dumps X^_k's spectrum and
             // A += fc^2 Re(sum_p conj(X^_k) R_k)
             if (int e = grow_fwd(xbk, spec, twW, W, rows, s)) return e;
-            if (int e = gcol(spec, xspec, fcT, at<cf>(ws, Lo.mT), twH, H, W, P, 0, s)) return e;
-            if (int e = grow_inv(spec, rb, twW, W, rows, s)) return e;
+            if (int e = gcol<T>(spec, xspec, fcT, at<C>(ws, Lo.mT), twH, H, W, P, 0, s)) return e;
+            if (int e = grow_inv<T>(spec, rb, twW, W, rows, s)) return e;
             if (psf_grad) {
-                hipLaunchKernelGGL(k_gxspec_acc, fgrid, fblk, 0, s, xspec, ht(k), P, H, Wh, fcT, at<double2>(ws, BL.aacc));
+                hipLaunchKernelGGL(k_gxspec_acc<T>, fgrid, fblk, 0, s, xspec, ht(k), P, H, Wh, fcT, at<double2>(ws, BL.aacc));
                 if (int e = launch_check("k_gxspec_acc")) return e;
             }
         }
@@ -1392,20 +1471,20 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xi
             ProfScope ps(2, s);
             const dim3 grid((unsigned)((HW + 255) / 256)), blk(256);
             if (lastk)
-                hipLaunchKernelGGL(k_giso_q<true>, grid, blk, 0, s, rb, ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0),
+                hipLaunchKernelGGL((k_giso_q<true, T>), grid, blk, 0, s, rb, ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0),
                                    ha(k - 1, 1), rho, q, H, W, P);
             else
-                hipLaunchKernelGGL(k_giso_q<false>, grid, blk, 0, s, rb, ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0),
+                hipLaunchKernelGGL((k_giso_q<false, T>), grid, blk, 0, s, rb, ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0),
                                    ha(k - 1, 1), rho, q, H, W, P);
             if (int e = launch_check("k_giso_q")) return e;
-            hipLaunchKernelGGL(k_iso_tau_partial, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
+            hipLaunchKernelGGL(k_iso_tau_partial<T>, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
                                tpart + (size_t)(K - k) * BL.ntp, 2LL * HW);
             if (int e = launch_check("k_iso_tau_partial")) return e;
-            allreduce(d, q, 2ull * H * W, s);
+            allreduce(d, reinterpret_cast<float*>(q), 2ull * H * W, s);
         }
         {
             ProfScope ps(0, s);
-            GBwdArgs ba{rb, xbuf[xo], bbar,
+            GBwdArgsT<T> ba{rb, xbuf[xo], bbar,
                         ab[2 * ain], ab[2 * ain + 1], ab[2 * (1 - ain)], ab[2 * (1 - ain) + 1],
                         ha(k, 0), ha(k, 1),
                         firstk ? nullptr : ha(k - 1, 0), firstk ? nullptr : ha(k - 1, 1),
@@ -1418,7 +1497,7 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xi
         ain = 1 - ain;
     }
     if (glam && grho) {
-        hipLaunchKernelGGL(k_bwd_scalars, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, BL.nstrips, 0LL,
+        hipLaunchKernelGGL(k_bwd_scalars<T>, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, BL.nstrips, 0LL,
                            d.iso ? tpart : nullptr, BL.ntp, 1, 0, lam, rho, glam, grho);
         if (int e = launch_check("k_bwd_scalars")) return e;
     } else if (glam || grho) {
@@ -1426,18 +1505,71 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const float* xi
     }
     if (psf_grad) {  // Z = sum_p conj(Bbar_p) Xin_p, then the k x k taps
         if (int e = grow_fwd(bbar, spec, twW, W, rows, s)) return e;
-        if (int e = gcol(spec, xspec, nullptr, nullptr, twH, H, W, P, 3, s)) return e;
+        if (int e = gcol<T>(spec, xspec, nullptr, nullptr, twH, H, W, P, 3, s)) return e;
         if (int e = grow_fwd(xin, spec, twW, W, rows, s)) return e;
-        if (int e = gcol(spec, spec, nullptr, nullptr, twH, H, W, P, 3, s)) return e;
-        hipLaunchKernelGGL(k_gxspec_acc, fgrid, fblk, 0, s, xspec, spec, P, H, Wh, nullptr, at<double2>(ws, BL.zacc));
+        if (int e = gcol<T>(spec, spec, nullptr, nullptr, twH, H, W, P, 3, s)) return e;
+        hipLaunchKernelGGL(k_gxspec_acc<T>, fgrid, fblk, 0, s, xspec, spec, P, H, Wh, nullptr, at<double2>(ws, BL.zacc));
         if (int e = launch_check("k_gxspec_acc")) return e;
-        hipLaunchKernelGGL(k_psf_grad, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
+        hipLaunchKernelGGL(k_psf_grad<T>, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
                            at<double2>(ws, BL.zacc), at<double2>(ws, Lo.sigma), d.kh, H, W, gkern, 1.0);
         if (int e = launch_check("k_psf_grad")) return e;
     }
     if (gxin && d.kh > 0)  // x^_in = H_t^T b^
-        if (int e = gapply(bbar, gxin, spec, Lo, ws, d, 2, s)) return e;
+        if (int e = gapply<T>(bbar, gxin, spec, Lo, ws, d, 2, s)) return e;
     return 0;
+}
+
+// ------------------------------------------------------------------ fp64 solves (ADMM_TV_FLAG_F64)
+// The forward of an fp64 solve: run_forward's contract on the generic kernels' double instantiation.
+int run_forward_f64(const admm_tv_desc& d, const double* xin, const double* kern, const double* lam,
+                    const double* rho, double* out, void* ws, size_t ws_bytes, void* hist, hipStream_t s) {
+    const Layout Lo = make_layout(d);
+    if (!ws || ws_bytes < Lo.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
+        return fail(ADMM_TV_EWORKSPACE, "workspace too small or not 256-byte aligned");
+    const int H = (int)d.H, W = (int)d.W;
+    const size_t img_bytes = (size_t)d.B * d.C * H * W * sizeof(double);
+    if (d.maxit == 0) {
+        if (img_bytes) HIPCHK(hipMemsetAsync(out, 0, img_bytes, s));  // the reference returns x = zeros
+        return 0;
+    }
+    if (participate_only(d)) {  // the same reductions as the iso loop, contributing zeros
+        for (int it = 1; it <= d.maxit; ++it) {
+            if (it == d.maxit && !hist) break;
+            HIPCHK(hipMemsetAsync(at<double>(ws, Lo.nsq), 0, 2ull * H * W * sizeof(double), s));
+            allreduce(d, at<float>(ws, Lo.nsq), 2ull * H * W, s);
+        }
+        return 0;
+    }
+    if (int e = setup<double>(d, Lo, ws, kern, rho, s)) return e;
+    return run_forward_gen<double>(d, Lo, xin, lam, rho, out, ws, hist, s);
+}
+
+int run_backward_f64(const admm_tv_desc& d, const double* xin, const double* kern, const double* lam,
+                     const double* rho, const double* gout, const void* hist, size_t hist_bytes, double* gxin,
+                     double* glam, double* grho, double* gkern, void* ws, size_t ws_bytes, hipStream_t s) {
+    const BwdLayout BL = make_bwd_layout(d);
+    if (!ws || ws_bytes < BL.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
+        return fail(ADMM_TV_EWORKSPACE, "workspace too small or not 256-byte aligned");
+    const int H = (int)d.H, W = (int)d.W, K = d.maxit;
+    const size_t img_bytes = (size_t)d.B * d.C * H * W * sizeof(double);
+    if (gkern && (d.kh == 0 || !(d.flags & ADMM_TV_FLAG_PSF_GRAD) || (!xin && !participate_only(d))))
+        return fail(ADMM_TV_EINVAL, "gkern needs a PSF, ADMM_TV_FLAG_PSF_GRAD (forward and backward) and xin");
+    if ((glam == nullptr) != (grho == nullptr)) return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
+    if (K == 0 || participate_only(d)) {
+        if (participate_only(d) && K > 0)
+            for (int k = K; k >= 2; --k) {
+                HIPCHK(hipMemsetAsync(at<double>(ws, BL.q), 0, 2ull * H * W * sizeof(double), s));
+                allreduce(d, at<float>(ws, BL.q), 2ull * H * W, s);
+            }
+        if (gxin && img_bytes) HIPCHK(hipMemsetAsync(gxin, 0, img_bytes, s));
+        if (glam) HIPCHK(hipMemsetAsync(glam, 0, sizeof(double), s));
+        if (grho) HIPCHK(hipMemsetAsync(grho, 0, sizeof(double), s));
+        if (gkern) HIPCHK(hipMemsetAsync(gkern, 0, sizeof(double) * d.kh * d.kw, s));
+        return 0;
+    }
+    if (!hist || hist_bytes < make_hist(d).total) return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
+    if (int e = setup<double>(d, BL.f, ws, kern, rho, s)) return e;
+    return run_backward_gen<double>(d, BL, xin, lam, rho, gout, hist, gxin, glam, grho, gkern, ws, s);
 }
 
 }  // namespace
@@ -1448,6 +1580,8 @@ extern "C" {
 int admm_tv_abi_version(void) { return ADMM_TV_ABI_VERSION; }
 
 int admm_tv_supported(int64_t H, int64_t W) { return supported_hw(H, W) ? 1 : generic_hw(H, W) ? 2 : 0; }
+
+int admm_tv_supported_f64(int64_t H, int64_t W) { return f64_hw(H, W) ? 1 : 0; }
 
 const char* admm_tv_last_error(void) { return g_err.c_str(); }
 
@@ -1461,6 +1595,7 @@ int admm_tv_workspace_size(const admm_tv_desc* d, size_t* bytes) {
 int admm_tv_forward(const admm_tv_desc* dp, const float* xin, const float* kern, const float* lam, const float* rho,
                     float* out, void* ws, size_t ws_bytes, void* stream) {
     if (int e = validate(dp)) return e;
+    if (is_f64(*dp)) return fail(ADMM_TV_EINVAL, "ADMM_TV_FLAG_F64: use admm_tv_forward_f64");
     if (((!xin || !out) && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
         return fail(ADMM_TV_EINVAL, "null pointer argument");
     DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
@@ -1479,6 +1614,7 @@ int admm_tv_forward_train(const admm_tv_desc* dp, const float* xin, const float*
                           const float* rho, float* out, void* hist, size_t hist_bytes, void* ws, size_t ws_bytes,
                           void* stream) {
     if (int e = validate(dp)) return e;
+    if (is_f64(*dp)) return fail(ADMM_TV_EINVAL, "ADMM_TV_FLAG_F64: use admm_tv_forward_train_f64");
     if (((!xin || !out) && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
         return fail(ADMM_TV_EINVAL, "null pointer argument");
     if (dp->maxit > 0 && (!hist || hist_bytes < make_hist(*dp).total))
@@ -1500,6 +1636,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
                      const float* rho, const float* gout, const void* hist, size_t hist_bytes, float* gxin,
                      float* glam, float* grho, float* gkern, void* ws, size_t ws_bytes, void* stream) {
     if (int e = validate(dp)) return e;
+    if (is_f64(*dp)) return fail(ADMM_TV_EINVAL, "ADMM_TV_FLAG_F64: use admm_tv_backward_f64");
     const admm_tv_desc d = *dp;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
@@ -1594,7 +1731,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
                 if ((e = launch_check("k_iso_reduce"))) return e;
                 // tau^ partial from this rank's Q (the norm N is already global): summing the
                 // ranks' lambda/rho gradients then counts every plane once
-                hipLaunchKernelGGL(k_iso_tau_partial, dim3(BL.ntp), dim3(256), 0, s, qg,
+                hipLaunchKernelGGL(k_iso_tau_partial<float>, dim3(BL.ntp), dim3(256), 0, s, qg,
                                    hn(k - 1) + (size_t)g * 2 * H * W, lam + g, rho + g,
                                    tpart + ((size_t)(K - k) * G + g) * BL.ntp, 2LL * H * W);
                 if ((e = launch_check("k_iso_tau_partial"))) return e;
@@ -1618,7 +1755,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     if (glam && grho) {
         const long long spm = BL.nstrips / G;  // strips of one module (module-major planes)
         for (int g = 0; g < G; ++g) {
-            hipLaunchKernelGGL(k_bwd_scalars, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, spm, (long long)g * spm,
+            hipLaunchKernelGGL(k_bwd_scalars<float>, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, spm, (long long)g * spm,
                                d.iso ? tpart : nullptr, BL.ntp, G, g, lam + g, rho + g, glam + g, grho + g);
             if ((e = launch_check("k_bwd_scalars"))) return e;
         }
@@ -1632,7 +1769,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
         hipLaunchKernelGGL(k_xspec_reduce, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, at<cf>(ws, BL.xpart),
                            BL.xgroups, nf, nullptr, at<double2>(ws, BL.zacc));
         if ((e = launch_check("k_xspec_reduce"))) return e;
-        hipLaunchKernelGGL(k_psf_grad, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
+        hipLaunchKernelGGL(k_psf_grad<float>, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
                            at<double2>(ws, BL.zacc), at<double2>(ws, Lo.sigma), d.kh, H, W, gkern, 0.25);
         if ((e = launch_check("k_psf_grad"))) return e;
     }
@@ -1653,6 +1790,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
 int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float* kern, float* out, void* ws,
                           size_t ws_bytes, void* stream) {
     if (int e = validate(dp)) return e;
+    if (is_f64(*dp)) return fail(ADMM_TV_EINVAL, "ADMM_TV_FLAG_F64: fp32 entry point");
     const admm_tv_desc d = *dp;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
@@ -1665,16 +1803,55 @@ int admm_tv_psf_transpose(const admm_tv_desc* dp, const float* xin, const float*
         HIPCHK(hipMemcpyAsync(out, xin, (size_t)P * H * W * sizeof(float), hipMemcpyDeviceToDevice, s));
         return 0;
     }
-    if (int e = setup(d, Lo, ws, kern, nullptr, s)) return e;
+    if (int e = setup<float>(d, Lo, ws, kern, nullptr, s)) return e;
     const int n = (N + 1) * H;
     // k_spectra needs a rho pointer: point it at a zeroed float inside the workspace (fcT region)
     HIPCHK(hipMemsetAsync(at<float>(ws, Lo.fcT), 0, sizeof(float), s));
-    hipLaunchKernelGGL(k_spectra, dim3((n + 255) / 256), dim3(256), 0, s, at<double2>(ws, Lo.G),
+    hipLaunchKernelGGL(k_spectra<float>, dim3((n + 255) / 256), dim3(256), 0, s, at<double2>(ws, Lo.G),
                        at<double2>(ws, Lo.twHd), at<float>(ws, Lo.fcT), at<float>(ws, Lo.spec[1]),
                        at<cf>(ws, Lo.mT), d.kh, H, N, W, nullptr, spectra_scale(H, W));
     if (int e = launch_check("k_spectra")) return e;
     if (Lo.gen) return gapply(xin, out, at<cf>(ws, Lo.spec[0]), Lo, ws, d, 1, s);
     return psf_transpose_into(d, Lo, ws, xin, out, at<cf>(ws, Lo.spec[0]), 1, s);
+}
+
+int admm_tv_forward_f64(const admm_tv_desc* dp, const double* xin, const double* kern, const double* lam,
+                        const double* rho, double* out, void* ws, size_t ws_bytes, void* stream) {
+    if (int e = validate(dp)) return e;
+    if (!is_f64(*dp)) return fail(ADMM_TV_EINVAL, "admm_tv_forward_f64 needs ADMM_TV_FLAG_F64");
+    if (((!xin || !out) && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
+        return fail(ADMM_TV_EINVAL, "null pointer argument");
+    DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
+    if (dg.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("device of the stream: ") + hipGetErrorString(dg.err));
+    return run_forward_f64(*dp, xin, kern, lam, rho, out, ws, ws_bytes, nullptr, reinterpret_cast<hipStream_t>(stream));
+}
+
+int admm_tv_forward_train_f64(const admm_tv_desc* dp, const double* xin, const double* kern, const double* lam,
+                              const double* rho, double* out, void* hist, size_t hist_bytes, void* ws, size_t ws_bytes,
+                              void* stream) {
+    if (int e = validate(dp)) return e;
+    if (!is_f64(*dp)) return fail(ADMM_TV_EINVAL, "admm_tv_forward_train_f64 needs ADMM_TV_FLAG_F64");
+    if (((!xin || !out) && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
+        return fail(ADMM_TV_EINVAL, "null pointer argument");
+    if (dp->maxit > 0 && (!hist || hist_bytes < make_hist(*dp).total))
+        return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
+    DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
+    if (dg.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("device of the stream: ") + hipGetErrorString(dg.err));
+    return run_forward_f64(*dp, xin, kern, lam, rho, out, ws, ws_bytes, dp->maxit > 0 ? hist : nullptr,
+                           reinterpret_cast<hipStream_t>(stream));
+}
+
+int admm_tv_backward_f64(const admm_tv_desc* dp, const double* xin, const double* kern, const double* lam,
+                         const double* rho, const double* gout, const void* hist, size_t hist_bytes, double* gxin,
+                         double* glam, double* grho, double* gkern, void* ws, size_t ws_bytes, void* stream) {
+    if (int e = validate(dp)) return e;
+    if (!is_f64(*dp)) return fail(ADMM_TV_EINVAL, "admm_tv_backward_f64 needs ADMM_TV_FLAG_F64");
+    if ((!gout && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
+        return fail(ADMM_TV_EINVAL, "null pointer argument");
+    DeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
+    if (dg.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("device of the stream: ") + hipGetErrorString(dg.err));
+    return run_backward_f64(*dp, xin, kern, lam, rho, gout, hist, hist_bytes, gxin, glam, grho, gkern, ws, ws_bytes,
+                            reinterpret_cast<hipStream_t>(stream));
 }
 
 int admm_tv_profile_enable(int enable) {

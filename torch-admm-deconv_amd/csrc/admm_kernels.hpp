@@ -95,29 +95,49 @@ __device__ __forceinline__ float block_factor(float sumsq, float tau) {
     float f = 1.f - tau / (n + 1e-15f);
     return f < 0.f ? 0.f : f;
 }
+// the reference's 1e-15 (deconv.py:20,24) in the solve's precision
+template <class T> __device__ __forceinline__ constexpr T eps15() {
+    if constexpr (std::is_same<T, float>::value) return 1e-15f;
+    else return 1e-15;
+}
+// fp64 (the generic kernels' double instantiation)
+__device__ __forceinline__ double soft(double a, double tau) {
+    double m = fabs(a) - tau;
+    m = (m < 0.0) ? 0.0 : m;
+    return copysign(m, a);
+}
+__device__ __forceinline__ double block_factor(double sumsq, double tau) {
+    double n = sqrt(sumsq + 1e-15);
+    double f = 1.0 - tau / (n + 1e-15);
+    return f < 0.0 ? 0.0 : f;
+}
 
 // ---------------------------------------------------------------------------
 // setup kernels
 // ---------------------------------------------------------------------------
 // twiddle tables: twW[k] = exp(-2 pi i k/W) (k < W), twH[k] = exp(-2 pi i k/H) (k < H),
 // twHd in fp64 for the PSF spectrum.
-__global__ void k_tables(cf* __restrict__ twW, cf* __restrict__ twH, double2* __restrict__ twHd, int H, int W) {
+// (C = cd: the fp64 solve keeps the tables in fp64)
+template <class C = cf>
+__global__ void k_tables(C* __restrict__ twW, C* __restrict__ twH, double2* __restrict__ twHd, int H, int W) {
+    using T = re_t<C>;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < W) {
         double s, c;
         sincospi(2.0 * i / W, &s, &c);
-        twW[i] = mkc((float)c, (float)-s);
+        twW[i] = mkx<T>((T)c, (T)-s);
     }
     if (i < H) {
         double s, c;
         sincospi(2.0 * i / H, &s, &c);
-        twH[i] = mkc((float)c, (float)-s);
+        twH[i] = mkx<T>((T)c, (T)-s);
         twHd[i] = make_double2(c, -s);
     }
 }
 
 // G[a][kx] = sum_b kern[a][b] exp(-2 pi i b kx / W), kx in [0, N], in fp64
-__global__ void k_psf_rows(const float* __restrict__ kern, double2* __restrict__ G, int k, int N, int W) {
+template <class T = float>
+__global__ void k_psf_rows(const T* __restrict__ kern, double2* __restrict__ G, int k, int N, int W) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= k * (N + 1)) return;
     const int a = i / (N + 1), kx = i % (N + 1);
@@ -136,8 +156,9 @@ __global__ void k_psf_rows(const float* __restrict__ kern, double2* __restrict__
 // fcT[kx][ky] = scale / (|sigma|^2 + rho (|Dx^|^2 + |Dy^|^2));
 // mT[kx][ky] = scale * sigma * exp(+2 pi i c (ky/H + kx/W))  (centred PSF, c = k/2)
 // scale = 1/(2HW) for the packed power-of-two path, 1/(HW) for the generic path
+template <class T = float>
 __global__ void k_spectra(const double2* __restrict__ G, const double2* __restrict__ twHd,
-                          const float* __restrict__ rho_p, float* __restrict__ fcT, cf* __restrict__ mT, int k,
+                          const T* __restrict__ rho_p, T* __restrict__ fcT, cx_t<T>* __restrict__ mT, int k,
                           int H, int N, int W, double2* __restrict__ sigma_out, double scale) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (N + 1) * H) return;
@@ -156,14 +177,14 @@ __global__ void k_spectra(const double2* __restrict__ G, const double2* __restri
     const double rho = (double)rho_p[0];
     const double sx = sinpi((double)kx / W), sy = sinpi((double)ky / H);
     const double lap = 4.0 * sx * sx + 4.0 * sy * sy;
-    fcT[i] = (float)(scale / (sr * sr + si * si + rho * lap));
+    fcT[i] = (T)(scale / (sr * sr + si * si + rho * lap));
     if (k > 0) {
         const int c = k / 2;  // ceil((k-1)/2): anchor of the reference's H_t
         const long long ph = (long long)c * ky * W + (long long)c * kx * H;  // units of 1/(H W)
         const long long HW = (long long)H * W;
         double s, co;
         sincospi(2.0 * (double)(ph % HW) / (double)HW, &s, &co);
-        mT[i] = mkc((float)((sr * co - si * s) * scale), (float)((sr * s + si * co) * scale));
+        mT[i] = mkx<T>((T)((sr * co - si * s) * scale), (T)((sr * s + si * co) * scale));
     }
 }
 
@@ -609,7 +630,7 @@ struct PassAArgs {
 #endif
 #define PASSA_MINW(n) ((n) >= 1024 ? 1 : PASSA_MINW_SMALL)
 
-template <bool ISO> __device__ __forceinline__ float shrink_z(float a, float tau, float nsum) {
+template <bool ISO, class T> __device__ __forceinline__ T shrink_z(T a, T tau, T nsum) {
     if constexpr (ISO) return block_factor(nsum, tau) * a;
     else return soft(a, tau);
 }

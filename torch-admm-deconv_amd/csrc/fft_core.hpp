@@ -45,6 +45,35 @@ template <int DIR> __device__ __forceinline__ cf mul_i(cf a) {
     return DIR < 0 ? mkc(a.y, -a.x) : mkc(-a.y, a.x);
 }
 
+// fp64 complex values (the generic kernels' double instantiation: fp64 inputs are solved in fp64,
+// as the reference computes in xin.dtype).  Same operation order as the fp32 helpers above.
+typedef double2 cd;
+__device__ __forceinline__ cd mkcd(double r, double i) { cd z; z.x = r; z.y = i; return z; }
+__device__ __forceinline__ cd cadd(cd a, cd b) { return mkcd(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ cd csub(cd a, cd b) { return mkcd(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ cd cmul(cd a, cd b) { return mkcd(fma(a.x, b.x, -(a.y * b.y)), fma(a.x, b.y, a.y * b.x)); }
+__device__ __forceinline__ cd cmulc(cd a, cd b) { return mkcd(fma(a.x, b.x, a.y * b.y), fma(a.y, b.x, -(a.x * b.y))); }
+__device__ __forceinline__ cd cconj(cd a) { return mkcd(a.x, -a.y); }
+__device__ __forceinline__ cd cscale(cd a, double s) { return mkcd(a.x * s, a.y * s); }
+template <int DIR> __device__ __forceinline__ cd mul_i(cd a) { return DIR < 0 ? mkcd(a.y, -a.x) : mkcd(-a.y, a.x); }
+
+// real type -> complex type, and a constructor usable from code templated on the real type
+template <class T> struct CxOf;
+template <> struct CxOf<float> { using type = cf; };
+template <> struct CxOf<double> { using type = cd; };
+template <class T> using cx_t = typename CxOf<T>::type;
+template <class T> __device__ __forceinline__ cx_t<T> mkx(T r, T i) {
+    if constexpr (std::is_same<T, float>::value) return mkc(r, i);
+    else return mkcd(r, i);
+}
+// the real type of a complex type (cf -> float, cd -> double)
+template <class C> struct ReOf;
+template <> struct ReOf<cf> { using type = float; };
+template <> struct ReOf<cd> { using type = double; };
+template <class C> using re_t = typename ReOf<C>::type;
+__device__ __forceinline__ float fmat(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ double fmat(double a, double b, double c) { return fma(a, b, c); }
+
 // cos(2*pi*m/64) for m in [0,16] with exact 0 at m = 16
 __device__ __forceinline__ constexpr double cos64q(int m) {
     constexpr double Q[17] = {1.0, 0.99518472667219693, 0.98078528040323043, 0.95694033573220882,

@@ -16,6 +16,11 @@
 //
 // Layouts: images float [P][H][W]; spectra cf [P][H][Wh]; multipliers transposed [Wh][H]
 // (k_spectra's layout with N = W/2, so the setup kernels are shared with the fast path).
+//
+// Precision: every kernel is templated on its real type T (float, or double for fp64 inputs, which
+// the reference computes in fp64: deconv.py:49,61-67,104-106); C = cx_t<T> is the complex type.
+// The double instantiation runs plans without Bluestein stages and with the generic (table
+// twiddle) butterflies for radices 8 and 16; the float code is unchanged by the templating.
 #pragma once
 #include "admm_backward.hpp"
 
@@ -53,9 +58,9 @@ __host__ __device__ constexpr int blue_e(int M) { return M <= 32 ? 4 : M <= 512 
 // one Stockham stage over `lines` transforms of length n held in LDS as [i][lines]
 // (element i of line c at src[i * lines + c]); threads stride over (line, vt) pairs.
 // ---------------------------------------------------------------------------
-template <int DIR>
-__device__ __forceinline__ cf twid(const cf* __restrict__ tw, int idx) {
-    const cf w = tw[idx];
+template <int DIR, class C>
+__device__ __forceinline__ C twid(const C* __restrict__ tw, int idx) {
+    const C w = tw[idx];
     return DIR < 0 ? w : cconj(w);
 }
 
@@ -75,20 +80,14 @@ template <int R> struct OddTw;
 template <> struct OddTw<3> {
     static constexpr double C[2] = {1.0, -0.5};
     static constexpr double S[2] = {0.0, 0.86602540378443864676};
-    static constexpr float cosv(int m) { return (float)C[m <= 1 ? m : 3 - m]; }
-    static constexpr float sinv(int m) { return (float)(m <= 1 ? S[m] : -S[3 - m]); }
 };
 template <> struct OddTw<5> {
     static constexpr double C[3] = {1.0, 0.30901699437494742410, -0.80901699437494742410};
     static constexpr double S[3] = {0.0, 0.95105651629515357212, 0.58778525229247312917};
-    static constexpr float cosv(int m) { return (float)C[m <= 2 ? m : 5 - m]; }
-    static constexpr float sinv(int m) { return (float)(m <= 2 ? S[m] : -S[5 - m]); }
 };
 template <> struct OddTw<7> {
     static constexpr double C[4] = {1.0, 0.62348980185873353053, -0.22252093395631440429, -0.90096886790241912624};
     static constexpr double S[4] = {0.0, 0.78183148246802980871, 0.97492791218182360702, 0.43388373911755812048};
-    static constexpr float cosv(int m) { return (float)C[m <= 3 ? m : 7 - m]; }
-    static constexpr float sinv(int m) { return (float)(m <= 3 ? S[m] : -S[7 - m]); }
 };
 
 template <> struct OddTw<11> {
@@ -96,60 +95,65 @@ template <> struct OddTw<11> {
                                     -0.654860733945285, -0.9594929736144974};
     static constexpr double S[6] = {0.0, 0.5406408174555976, 0.9096319953545183, 0.9898214418809328,
                                     0.7557495743542583, 0.28173255684142967};
-    static constexpr float cosv(int m) { return (float)C[m <= 5 ? m : 11 - m]; }
-    static constexpr float sinv(int m) { return (float)(m <= 5 ? S[m] : -S[11 - m]); }
 };
 template <> struct OddTw<13> {
     static constexpr double C[7] = {1.0, 0.8854560256532099, 0.5680647467311559, 0.120536680255323,
                                     -0.35460488704253545, -0.7485107481711012, -0.970941817426052};
     static constexpr double S[7] = {0.0, 0.4647231720437685, 0.8229838658936564, 0.992708874098054,
                                     0.9350162426854148, 0.6631226582407952, 0.23931566428755768};
-    static constexpr float cosv(int m) { return (float)C[m <= 6 ? m : 13 - m]; }
-    static constexpr float sinv(int m) { return (float)(m <= 6 ? S[m] : -S[13 - m]); }
 };
 
-template <int DIR, int R>
-__device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw, int n) {
+// cos / sin(2 pi m / R) in the real type T ((float)C[...] for T = float, as cosv / sinv)
+template <int R, class T> __device__ __forceinline__ constexpr T odd_cos(int m) {
+    return (T)OddTw<R>::C[m <= (R - 1) / 2 ? m : R - m];
+}
+template <int R, class T> __device__ __forceinline__ constexpr T odd_sin(int m) {
+    return (T)(m <= (R - 1) / 2 ? OddTw<R>::S[m] : -OddTw<R>::S[R - m]);
+}
+
+template <int DIR, int R, class C>
+__device__ __forceinline__ void small_dft(C (&v)[R], const C* __restrict__ tw, int n) {
+    using T = re_t<C>;
     if constexpr (R == 2) {
-        const cf a = v[0], b = v[1];
+        const C a = v[0], b = v[1];
         v[0] = cadd(a, b);
         v[1] = csub(a, b);
     } else if constexpr (R == 4) {
-        const cf t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]), t2 = cadd(v[1], v[3]);
-        const cf t3 = mul_i<DIR>(csub(v[1], v[3]));
+        const C t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]), t2 = cadd(v[1], v[3]);
+        const C t3 = mul_i<DIR>(csub(v[1], v[3]));
         v[0] = cadd(t0, t2);
         v[2] = csub(t0, t2);
         v[1] = cadd(t1, t3);
         v[3] = csub(t1, t3);
-    } else if constexpr (R == 8 || R == 16) {
+    } else if constexpr ((R == 8 || R == 16) && std::is_same<T, float>::value) {
         DFT<R, DIR>::template run<1, 0>(v);  // register DFT with exact constant twiddles (fft_core.hpp)
     } else if constexpr (R == 3 || R == 5 || R == 7 || R == 11 || R == 13) {
         // odd R with compile-time cosines / sines on the input sums / differences (the pairing of
         // gstage_any): y_k, y_{R-k} = x0 + sum_q s_q cos(qk) -+ DIR i sum_q d_q sin(qk)
         constexpr int h = (R - 1) / 2;
-        cf s[h + 1], d[h + 1];
-        cf y0 = v[0];
+        C s[h + 1], d[h + 1];
+        C y0 = v[0];
         static_for<1, h + 1>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             s[q] = cadd(v[q], v[R - q]);
             d[q] = csub(v[q], v[R - q]);
             y0 = cadd(y0, s[q]);
         });
-        cf out[R];
+        C out[R];
         out[0] = y0;
         static_for<1, h + 1>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            cf a = v[0], b = mkc(0.f, 0.f);
+            C a = v[0], b = mkx<T>(0, 0);
             static_for<1, h + 1>([&](auto qc) {
                 constexpr int q = decltype(qc)::value;
-                constexpr float c = OddTw<R>::cosv((q * k) % R), sn = OddTw<R>::sinv((q * k) % R);
-                a.x = fmaf(s[q].x, c, a.x);
-                a.y = fmaf(s[q].y, c, a.y);
-                b.x = fmaf(d[q].x, sn, b.x);
-                b.y = fmaf(d[q].y, sn, b.y);
+                constexpr T c = odd_cos<R, T>((q * k) % R), sn = odd_sin<R, T>((q * k) % R);
+                a.x = fmat(s[q].x, c, a.x);
+                a.y = fmat(s[q].y, c, a.y);
+                b.x = fmat(d[q].x, sn, b.x);
+                b.y = fmat(d[q].y, sn, b.y);
             });
             // i b = (-b.y, b.x); forward (DIR < 0): y_k = a - i b
-            const cf ib = mkc(-b.y, b.x);
+            const C ib = mkx<T>(-b.y, b.x);
             out[k] = DIR < 0 ? csub(a, ib) : cadd(a, ib);
             out[R - k] = DIR < 0 ? cadd(a, ib) : csub(a, ib);
         });
@@ -159,15 +163,15 @@ __device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw,
         (void)n;
     } else {
         // y_k = sum_q v_q W_R^{qk}, W_R^j = tw[j n / R]
-        cf y[R];
+        C y[R];
         const int step = n / R;
 #pragma unroll
         for (int k = 0; k < R; ++k) {
-            cf acc = v[0];
+            C acc = v[0];
 #pragma unroll
             for (int q = 1; q < R; ++q) {
-                const cf w = twid<DIR>(tw, ((q * k) % R) * step);
-                const cf p = cmul(v[q], w);
+                const C w = twid<DIR>(tw, ((q * k) % R) * step);
+                const C p = cmul(v[q], w);
                 acc = cadd(acc, p);
             }
             y[k] = acc;
@@ -177,9 +181,9 @@ __device__ __forceinline__ void small_dft(cf (&v)[R], const cf* __restrict__ tw,
     }
 }
 
-template <int DIR, int R>
-__device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restrict__ dst, int n, int NS, int lines,
-                                         const cf* __restrict__ tw) {
+template <int DIR, int R, class C>
+__device__ __forceinline__ void gstage_r(const C* __restrict__ src, C* __restrict__ dst, int n, int NS, int lines,
+                                         const C* __restrict__ tw) {
     const int nb = n / R;                 // butterflies per line
     const int tstride = n / (NS * R);     // twiddle index stride of W_{NS R}
     const int lg = __ffs(lines) - 1;      // lines is a power of two
@@ -187,10 +191,10 @@ __device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restr
     for (int item = threadIdx.x; item < nb * lines; item += blockDim.x) {
         const int c = item & (lines - 1), vt = item >> lg;
         const int vq = fdiv(vt, NS, rns), m = vt - vq * NS;
-        cf v[R];
+        C v[R];
 #pragma unroll
         for (int q = 0; q < R; ++q) {
-            cf x = src[(vt + q * nb) * lines + c];
+            C x = src[(vt + q * nb) * lines + c];
             if (q > 0 && m > 0) x = cmul(x, twid<DIR>(tw, m * q * tstride));
             v[q] = x;
         }
@@ -216,9 +220,10 @@ __device__ __forceinline__ void gstage_r(const cf* __restrict__ src, cf* __restr
 #endif
 constexpr int GP = ADMM_GP;
 
-template <int DIR>
-__device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict__ dst, int n, int NS, int R,
-                                           int lines, const cf* __restrict__ tw) {
+template <int DIR, class C>
+__device__ __forceinline__ void gstage_any(C* __restrict__ src, C* __restrict__ dst, int n, int NS, int R,
+                                           int lines, const C* __restrict__ tw) {
+    using T = re_t<C>;
     const int nb = n / R;
     const int span = NS * R;
     const int tstride = n / span;
@@ -230,7 +235,7 @@ __device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict_
             const int q = fdiv(o, nb, rnb), vt = o - q * nb;
             const int m = vt - fdiv(vt, NS, rns) * NS;
             if (q > 0 && m > 0) {
-                cf* x = src + (size_t)o * lines + c;
+                C* x = src + (size_t)o * lines + c;
                 *x = cmul(*x, twid<DIR>(tw, m * q * tstride));  // m q < NS R: no reduction
             }
         }
@@ -244,49 +249,49 @@ __device__ __forceinline__ void gstage_any(cf* __restrict__ src, cf* __restrict_
         const int g = fdiv(o, nb, rnb), vt = o - g * nb;
         const int vq = fdiv(vt, NS, rns), m = vt - vq * NS;
         const int k0 = 1 + g * GP;
-        const cf* col = src + (size_t)vt * lines + c;
+        const C* col = src + (size_t)vt * lines + c;
         const size_t qstep = (size_t)nb * lines;
-        cf x0 = col[0];
-        cf acc0 = x0;  // output 0 (group 0 only)
+        C x0 = col[0];
+        C acc0 = x0;  // output 0 (group 0 only)
         // inputs q and R - q share the twiddle pair w, conj(w) (w = W_R^{qk}):
         //   x_q w + x_{R-q} conj(w) = s w.x + i d w.y,   x_q conj(w) + x_{R-q} w = s w.x - i d w.y
         // with s = x_q + x_{R-q}, d = x_q - x_{R-q}: four FMAs per input pair for both outputs
         // k and R - k (the real cosine / sine sums), half the loop trips of the per-input form
-        cf sa[GP], sb[GP];  // sum s w.x, sum d w.y
+        C sa[GP], sb[GP];  // sum s w.x, sum d w.y
         int idx[GP];  // table index (q (k0 + j) mod R) * rstep, stepped without multiply or modulo
         const int wrap = R * rstep;
 #pragma unroll
         for (int j = 0; j < GP; ++j) {
-            sa[j] = mkc(0.f, 0.f);
-            sb[j] = mkc(0.f, 0.f);
+            sa[j] = mkx<T>(0, 0);
+            sb[j] = mkx<T>(0, 0);
             idx[j] = 0;
         }
 #pragma unroll ADMM_GUNROLL
         for (int q = 1; q <= npair; ++q) {
-            const cf xa = col[q * qstep], xb = col[(R - q) * qstep];
-            const cf s = cadd(xa, xb), d = csub(xa, xb);
+            const C xa = col[q * qstep], xb = col[(R - q) * qstep];
+            const C s = cadd(xa, xb), d = csub(xa, xb);
             acc0 = cadd(acc0, s);
 #pragma unroll
             for (int j = 0; j < GP; ++j) {
                 idx[j] += (k0 + j) * rstep;
                 if (idx[j] >= wrap) idx[j] -= wrap;
-                const cf w = twid<DIR>(tw, idx[j]);
-                sa[j].x = fmaf(s.x, w.x, sa[j].x);
-                sa[j].y = fmaf(s.y, w.x, sa[j].y);
-                sb[j].x = fmaf(d.x, w.y, sb[j].x);
-                sb[j].y = fmaf(d.y, w.y, sb[j].y);
+                const C w = twid<DIR>(tw, idx[j]);
+                sa[j].x = fmat(s.x, w.x, sa[j].x);
+                sa[j].y = fmat(s.y, w.x, sa[j].y);
+                sb[j].x = fmat(d.x, w.y, sb[j].x);
+                sb[j].y = fmat(d.y, w.y, sb[j].y);
             }
         }
-        cf* out = dst + ((size_t)vq * span + m) * lines + c;
+        C* out = dst + ((size_t)vq * span + m) * lines + c;
         const size_t kstep = (size_t)NS * lines;
         if (g == 0) out[0] = acc0;
 #pragma unroll
         for (int j = 0; j < GP; ++j) {
             const int k = k0 + j;
             if (k <= npair) {
-                const cf a = cadd(x0, sa[j]);
-                out[k * kstep] = mkc(a.x - sb[j].y, a.y + sb[j].x);        // a + i sb
-                out[(R - k) * kstep] = mkc(a.x + sb[j].y, a.y - sb[j].x);  // a - i sb
+                const C a = cadd(x0, sa[j]);
+                out[k * kstep] = mkx<T>(a.x - sb[j].y, a.y + sb[j].x);        // a + i sb
+                out[(R - k) * kstep] = mkx<T>(a.x + sb[j].y, a.y - sb[j].x);  // a - i sb
             }
         }
     }
@@ -349,16 +354,28 @@ __device__ __forceinline__ void gstage_blue(const cf* __restrict__ src, cf* __re
 // twiddles followed by the plan's Bluestein tables (LDS); xbuf: pl.xslots exchange slots.
 // BM: the plan's Bluestein size (a template parameter, so a kernel without Bluestein stages keeps
 // its small register footprint; each BM is its own kernel instantiation).
-template <int DIR, int BM>
-__device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf* __restrict__ tw,
-                        cf* __restrict__ xbuf) {  // bufA is clobbered
-    cf* src = bufA;
-    cf* dst = bufB;
+template <int DIR, int BM, class C>
+__device__ C* gfft_lds(C* bufA, C* bufB, const GPlan& pl, int lines, const C* __restrict__ tw,
+                       C* __restrict__ xbuf) {  // bufA is clobbered
+    static_assert(BM == 0 || std::is_same<C, cf>::value, "Bluestein stages: fp32 only");
+    C* src = bufA;
+    C* dst = bufB;
     int NS = 1;
     for (int s = 0; s < pl.nst; ++s) {
         const int R = pl.rad[s];
         if (BM > 0 && pl.bst[s] > 0) {
-            if constexpr (BM > 0) gstage_blue<DIR, BM>(src, dst, pl.n, NS, R, lines, tw, tw + pl.boff[s], xbuf);
+            if constexpr (BM > 0 && std::is_same<C, cf>::value)
+                gstage_blue<DIR, BM>(src, dst, pl.n, NS, R, lines, tw, tw + pl.boff[s], xbuf);
+        } else if constexpr (std::is_same<C, cd>::value) {
+            // fp64 plans: radices 4, 2, 3, 5 and the any-prime stage (make_plan_f64), which keeps the
+            // double kernels' register footprint bounded
+            switch (R) {
+                case 2: gstage_r<DIR, 2>(src, dst, pl.n, NS, lines, tw); break;
+                case 3: gstage_r<DIR, 3>(src, dst, pl.n, NS, lines, tw); break;
+                case 4: gstage_r<DIR, 4>(src, dst, pl.n, NS, lines, tw); break;
+                case 5: gstage_r<DIR, 5>(src, dst, pl.n, NS, lines, tw); break;
+                default: gstage_any<DIR>(src, dst, pl.n, NS, R, lines, tw); break;
+            }
         } else {
             switch (R) {
                 case 2: gstage_r<DIR, 2>(src, dst, pl.n, NS, lines, tw); break;
@@ -374,7 +391,7 @@ __device__ cf* gfft_lds(cf* bufA, cf* bufB, const GPlan& pl, int lines, const cf
             }
         }
         __syncthreads();
-        cf* t = src;
+        C* t = src;
         src = dst;
         dst = t;
         NS *= R;
@@ -430,71 +447,75 @@ __global__ void k_blue_tables(cf* __restrict__ tab, GPlan pl) {
 // ---------------------------------------------------------------------------
 // row transforms: `lines` rows per block (contiguous rows of one image set)
 // ---------------------------------------------------------------------------
-struct GRowArgs {
-    const float* img;  // fwd: input rows [rows][W];   inv: output rows
-    cf* spec;          // fwd: output [rows][Wh];       inv: input
-    float* img_out;
-    const cf* tw;      // [W]
+template <class T> struct GRowArgsT {
+    const T* img;        // fwd: input rows [rows][W];   inv: output rows
+    cx_t<T>* spec;       // fwd: output [rows][Wh];       inv: input
+    T* img_out;
+    const cx_t<T>* tw;   // [W]
     GPlan plan;
     long long rows;
-    int lines;         // rows per block
+    int lines;           // rows per block
 };
+using GRowArgs = GRowArgsT<float>;
 
 // Real rows are transformed two at a time: rows a, b as one complex row z = a + i b, whose
 // spectrum Z gives A[k] = (Z[k] + conj Z[-k]) / 2 and B[k] = (Z[k] - conj Z[-k]) / 2i.  A block
 // holds `lines` complex rows = 2 * lines real rows.
 // TWG: twiddles / tables read from global memory (GPlan::twg; a template parameter, so the LDS
 // variant keeps its LDS reads)
-template <int BM, bool TWG, int NT = GNT>
-__global__ void __launch_bounds__(NT) k_grow_fwd(GRowArgs a) {
+template <int BM, bool TWG, int NT = GNT, class T = float>
+__global__ void __launch_bounds__(NT) k_grow_fwd(GRowArgsT<T> a) {
+    using C = cx_t<T>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
-    cf* twl = reinterpret_cast<cf*>(smem);
-    cf* A = twl + (TWG ? 0 : W + a.plan.ntab);
-    cf* B = A + (size_t)W * lines;
-    cf* X = B + (size_t)W * lines;  // Bluestein exchange slots
+    C* twl = reinterpret_cast<C*>(smem);
+    C* A = twl + (TWG ? 0 : W + a.plan.ntab);
+    C* B = A + (size_t)W * lines;
+    C* X = B + (size_t)W * lines;  // Bluestein exchange slots
     if constexpr (!TWG)
         for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
-    const cf* tw = TWG ? a.tw : twl;
+    const C* tw = TWG ? a.tw : twl;
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);  // real rows in this block
     for (int rr = 0; rr < 2 * lines; ++rr)  // coalesced along the row
         for (int i = threadIdx.x; i < W; i += blockDim.x) {
-            const float v = rr < nl ? a.img[(r0 + rr) * W + i] : 0.f;
-            float* slot = reinterpret_cast<float*>(&A[i * lines + (rr >> 1)]);
+            const T v = rr < nl ? a.img[(r0 + rr) * W + i] : T(0);
+            T* slot = reinterpret_cast<T*>(&A[i * lines + (rr >> 1)]);
             slot[rr & 1] = v;  // even row -> real part, odd row -> imaginary part
         }
     __syncthreads();
-    const cf* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
+    const C* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
+    const T half = T(0.5);
     for (int c = 0; c < lines; ++c)
         for (int k = threadIdx.x; k < Wh; k += blockDim.x) {
-            const cf z = res[k * lines + c];
-            const cf m = res[(k == 0 ? 0 : W - k) * lines + c];
+            const C z = res[k * lines + c];
+            const C m = res[(k == 0 ? 0 : W - k) * lines + c];
             const long long ra = r0 + 2 * c;
-            if (2 * c < nl) a.spec[ra * Wh + k] = mkc(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));
-            if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkc(0.5f * (z.y + m.y), 0.5f * (m.x - z.x));
+            if (2 * c < nl) a.spec[ra * Wh + k] = mkx<T>(half * (z.x + m.x), half * (z.y - m.y));
+            if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkx<T>(half * (z.y + m.y), half * (m.x - z.x));
         }
 }
 
-template <int BM, bool TWG, int NT = GNT>
-__global__ void __launch_bounds__(NT) k_grow_inv(GRowArgs a) {
+template <int BM, bool TWG, int NT = GNT, class T = float>
+__global__ void __launch_bounds__(NT) k_grow_inv(GRowArgsT<T> a) {
+    using C = cx_t<T>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
-    cf* twl = reinterpret_cast<cf*>(smem);
-    cf* A = twl + (TWG ? 0 : W + a.plan.ntab);
-    cf* B = A + (size_t)W * lines;
-    cf* X = B + (size_t)W * lines;
+    C* twl = reinterpret_cast<C*>(smem);
+    C* A = twl + (TWG ? 0 : W + a.plan.ntab);
+    C* B = A + (size_t)W * lines;
+    C* X = B + (size_t)W * lines;
     if constexpr (!TWG)
         for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
-    const cf* tw = TWG ? a.tw : twl;
+    const C* tw = TWG ? a.tw : twl;
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);
     // Hermitian completion of a half spectrum: X[k] = conj X[W - k] for k >= Wh; the imaginary
     // parts of the self-conjugate bins (DC, and Nyquist for even W) are dropped, as irfft does
-    auto full = [&](long long row, int k) -> cf {
+    auto full = [&](long long row, int k) -> C {
         if (k < Wh) {
-            cf v = a.spec[row * Wh + k];
-            if (k == 0 || 2 * k == W) v.y = 0.f;
+            C v = a.spec[row * Wh + k];
+            if (k == 0 || 2 * k == W) v.y = T(0);
             return v;
         }
         return cconj(a.spec[row * Wh + (W - k)]);
@@ -502,15 +523,15 @@ __global__ void __launch_bounds__(NT) k_grow_inv(GRowArgs a) {
     for (int c = 0; c < lines; ++c)
         for (int k = threadIdx.x; k < W; k += blockDim.x) {
             const long long ra = r0 + 2 * c;
-            const cf xa = 2 * c < nl ? full(ra, k) : mkc(0.f, 0.f);
-            const cf xb = 2 * c + 1 < nl ? full(ra + 1, k) : mkc(0.f, 0.f);
-            A[k * lines + c] = mkc(xa.x - xb.y, xa.y + xb.x);  // Z = Xa + i Xb
+            const C xa = 2 * c < nl ? full(ra, k) : mkx<T>(0, 0);
+            const C xb = 2 * c + 1 < nl ? full(ra + 1, k) : mkx<T>(0, 0);
+            A[k * lines + c] = mkx<T>(xa.x - xb.y, xa.y + xb.x);  // Z = Xa + i Xb
         }
     __syncthreads();
-    const cf* res = gfft_lds<+1, BM>(A, B, a.plan, lines, tw, X);
+    const C* res = gfft_lds<+1, BM>(A, B, a.plan, lines, tw, X);
     for (int rr = 0; rr < nl; ++rr)
         for (int i = threadIdx.x; i < W; i += blockDim.x) {
-            const cf z = res[i * lines + (rr >> 1)];
+            const C z = res[i * lines + (rr >> 1)];
             a.img_out[(r0 + rr) * W + i] = (rr & 1) ? z.y : z.x;
         }
 }
@@ -521,18 +542,19 @@ __global__ void __launch_bounds__(NT) k_grow_inv(GRowArgs a) {
 // forward column spectrum to `dump` and stop; used for cross-spectra).  `dump` (MODE 0) also
 // receives the forward spectrum before the multiply when non-null.
 // ---------------------------------------------------------------------------
-struct GColArgs {
-    cf* spec;        // [P][H][Wh], in place
-    cf* dump;        // optional [P][H][Wh]
-    const float* fcT;
-    const cf* mT;
-    const cf* tw;    // [H]
-    GPlan plan;      // n = H
+template <class T> struct GColArgsT {
+    cx_t<T>* spec;        // [P][H][Wh], in place
+    cx_t<T>* dump;        // optional [P][H][Wh]
+    const T* fcT;
+    const cx_t<T>* mT;
+    const cx_t<T>* tw;    // [H]
+    GPlan plan;           // n = H
     int Wh;
-    int cols;        // columns per block
+    int cols;             // columns per block
     int colblocks;
     long long P;
 };
+using GColArgs = GColArgsT<float>;
 
 // occupancy hint of the column pass with Bluestein stages of size 256 (waves per SIMD; A/B knob
 // -DADMM_GCOL_MINW=4 caps its VGPRs at 128)
@@ -541,31 +563,32 @@ struct GColArgs {
 #endif
 constexpr int gcol_minw(int bm) { return bm == 256 ? ADMM_GCOL_MINW : 1; }
 
-template <int MODE, int BM, bool TWG, int NT = GNT>
-__global__ void __launch_bounds__(NT, gcol_minw(BM)) k_gcol(GColArgs a) {
+template <int MODE, int BM, bool TWG, int NT = GNT, class T = float>
+__global__ void __launch_bounds__(NT, gcol_minw(BM)) k_gcol(GColArgsT<T> a) {
+    using C = cx_t<T>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
     const int lgc = __ffs(cols) - 1;  // cols is a power of two
-    cf* twl = reinterpret_cast<cf*>(smem);
-    cf* A = twl + (TWG ? 0 : H + a.plan.ntab);
-    cf* B = A + (size_t)H * cols;
-    cf* X = B + (size_t)H * cols;
+    C* twl = reinterpret_cast<C*>(smem);
+    C* A = twl + (TWG ? 0 : H + a.plan.ntab);
+    C* B = A + (size_t)H * cols;
+    C* X = B + (size_t)H * cols;
     if constexpr (!TWG)
         for (int i = threadIdx.x; i < H + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
-    const cf* tw = TWG ? a.tw : twl;
+    const C* tw = TWG ? a.tw : twl;
     const long long p = blockIdx.x / a.colblocks;
     const int c0 = (int)(blockIdx.x % a.colblocks) * cols;
     const int nc = min(cols, Wh - c0);
-    cf* S = a.spec + (size_t)p * H * Wh + c0;
+    C* S = a.spec + (size_t)p * H * Wh + c0;
     for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
         const int i = idx >> lgc, c = idx & (cols - 1);  // coalesced across the block's columns
-        A[i * cols + c] = c < nc ? S[(size_t)i * Wh + c] : mkc(0.f, 0.f);
+        A[i * cols + c] = c < nc ? S[(size_t)i * Wh + c] : mkx<T>(0, 0);
     }
     __syncthreads();
-    cf* res = gfft_lds<-1, BM>(A, B, a.plan, cols, tw, X);
-    cf* other = (res == A) ? B : A;
+    C* res = gfft_lds<-1, BM>(A, B, a.plan, cols, tw, X);
+    C* other = (res == A) ? B : A;
     if (a.dump) {
-        cf* D = a.dump + (size_t)p * H * Wh + c0;
+        C* D = a.dump + (size_t)p * H * Wh + c0;
         for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
             const int i = idx >> lgc, c = idx & (cols - 1);
             if (c < nc) D[(size_t)i * Wh + c] = res[i * cols + c];
@@ -576,14 +599,14 @@ __global__ void __launch_bounds__(NT, gcol_minw(BM)) k_gcol(GColArgs a) {
         const int ky = idx >> lgc, c = idx & (cols - 1);
         if (c >= nc) continue;
         const size_t f = (size_t)(c0 + c) * H + ky;
-        cf v = res[ky * cols + c];
+        C v = res[ky * cols + c];
         if constexpr (MODE == 0) v = cscale(v, a.fcT[f]);
         else if constexpr (MODE == 1) v = cmul(v, a.mT[f]);
         else v = cmulc(v, a.mT[f]);
         res[ky * cols + c] = v;
     }
     __syncthreads();
-    const cf* out = gfft_lds<+1, BM>(res, other, a.plan, cols, tw, X);
+    const C* out = gfft_lds<+1, BM>(res, other, a.plan, cols, tw, X);
     for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
         const int i = idx >> lgc, c = idx & (cols - 1);
         if (c < nc) S[(size_t)i * Wh + c] = out[i * cols + c];
@@ -595,30 +618,30 @@ __global__ void __launch_bounds__(NT, gcol_minw(BM)) k_gcol(GColArgs a) {
 // neighbours is recomputed from the same inputs by the same expressions, so every pixel
 // sees exactly the values its neighbours compute for themselves.
 // ---------------------------------------------------------------------------
-struct GStepArgs {
-    const float* x;      // x_k                                   [P][H][W]
-    const float* b;      // H_t(xin)
-    const float* uxi;    // u_{k-1} (a_{k-1} when HIST)
-    const float* uyi;
-    float* uxo;          // u_k (a_k when HIST)
-    float* uyo;
-    float* r;            // r_{k+1} = b + rho D^T w_k (may be null: training's last iteration)
-    const float* nsq;    // iso: N_k  [2][H][W]
-    const float* nsq_prev;  // iso + HIST: N_{k-1}
-    const float* lam;
-    const float* rho;
+template <class T> struct GStepArgsT {
+    const T* x;          // x_k                                   [P][H][W]
+    const T* b;          // H_t(xin)
+    const T* uxi;        // u_{k-1} (a_{k-1} when HIST)
+    const T* uyi;
+    T* uxo;              // u_k (a_k when HIST)
+    T* uyo;
+    T* r;                // r_{k+1} = b + rho D^T w_k (may be null: training's last iteration)
+    const T* nsq;        // iso: N_k  [2][H][W]
+    const T* nsq_prev;   // iso + HIST: N_{k-1}
+    const T* lam;
+    const T* rho;
     int H, W;
     long long npx;       // P H W
 };
+using GStepArgs = GStepArgsT<float>;
 
-template <bool ISO, bool FIRST, bool HIST>
-__device__ __forceinline__ float gprev_u(const float* __restrict__ src, const float* __restrict__ np, size_t i, size_t hw,
-                                         float tau) {
+template <bool ISO, bool FIRST, bool HIST, class T>
+__device__ __forceinline__ T gprev_u(const T* __restrict__ src, const T* __restrict__ np, size_t i, size_t hw, T tau) {
     if constexpr (FIRST) {
-        return 0.f;
+        return T(0);
     } else {
-        const float v = src[i];
-        if constexpr (HIST) return v - shrink_z<ISO>(v, tau, ISO ? np[hw] : 0.f);
+        const T v = src[i];
+        if constexpr (HIST) return v - shrink_z<ISO>(v, tau, ISO ? np[hw] : T(0));
         else return v;
     }
 }
@@ -627,10 +650,10 @@ __device__ __forceinline__ float gprev_u(const float* __restrict__ src, const fl
 // (b + rho D^T w; unused when a.r is null in k_gstep)
 // (the image pointers as __restrict__ parameters: after inlining the compiler may move one
 // pixel's loads above another's stores, so a thread's pixels overlap their memory latency)
-template <bool ISO, bool FIRST, bool HIST>
-__device__ __forceinline__ float gstep_pxr(const GStepArgs& a, const float* __restrict__ xs, const float* __restrict__ bs,
-                                           const float* __restrict__ uxs, const float* __restrict__ uys,
-                                           float* __restrict__ uxd, float* __restrict__ uyd, unsigned row, int j) {
+template <bool ISO, bool FIRST, bool HIST, class T>
+__device__ __forceinline__ T gstep_pxr(const GStepArgsT<T>& a, const T* __restrict__ xs, const T* __restrict__ bs,
+                                       const T* __restrict__ uxs, const T* __restrict__ uys, T* __restrict__ uxd,
+                                       T* __restrict__ uyd, unsigned row, int j) {
     const int H = a.H, W = a.W;
     const int i = (int)(row % (unsigned)H);
     const long long pb = (long long)(row - (unsigned)i) * W;
@@ -641,18 +664,18 @@ __device__ __forceinline__ float gstep_pxr(const GStepArgs& a, const float* __re
     const int im = i == 0 ? H - 1 : i - 1, ip = i == H - 1 ? 0 : i + 1;
     const size_t P0 = (size_t)idx, PR = (size_t)(pb + (long long)i * W + jp), PD = (size_t)(pb + (long long)ip * W + j);
     const size_t h0 = (size_t)rem, hR = (size_t)i * W + jp, hD = (size_t)ip * W + j;
-    const float rho = a.rho[0];
-    const float tau = a.lam[0] / rho;
-    const float x = xs[P0];
-    const float xl = xs[pb + (long long)i * W + jm], xr = xs[PR];
-    const float xu = xs[pb + (long long)im * W + j], xd = xs[PD];
-    const float* npx = a.nsq_prev;
-    const float* npy = a.nsq_prev ? a.nsq_prev + HW : nullptr;
-    const float ux0 = gprev_u<ISO, FIRST, HIST>(uxs, npx, P0, h0, tau);
-    const float uxR = gprev_u<ISO, FIRST, HIST>(uxs, npx, PR, hR, tau);
-    const float uy0 = gprev_u<ISO, FIRST, HIST>(uys, npy, P0, h0, tau);
-    const float uyD = gprev_u<ISO, FIRST, HIST>(uys, npy, PD, hD, tau);
-    float nx0 = 0.f, nxR = 0.f, ny0 = 0.f, nyD = 0.f;
+    const T rho = a.rho[0];
+    const T tau = a.lam[0] / rho;
+    const T x = xs[P0];
+    const T xl = xs[pb + (long long)i * W + jm], xr = xs[PR];
+    const T xu = xs[pb + (long long)im * W + j], xd = xs[PD];
+    const T* npx = a.nsq_prev;
+    const T* npy = a.nsq_prev ? a.nsq_prev + HW : nullptr;
+    const T ux0 = gprev_u<ISO, FIRST, HIST>(uxs, npx, P0, h0, tau);
+    const T uxR = gprev_u<ISO, FIRST, HIST>(uxs, npx, PR, hR, tau);
+    const T uy0 = gprev_u<ISO, FIRST, HIST>(uys, npy, P0, h0, tau);
+    const T uyD = gprev_u<ISO, FIRST, HIST>(uys, npy, PD, hD, tau);
+    T nx0 = 0, nxR = 0, ny0 = 0, nyD = 0;
     if constexpr (ISO) {
         nx0 = a.nsq[h0];
         nxR = a.nsq[hR];
@@ -660,97 +683,99 @@ __device__ __forceinline__ float gstep_pxr(const GStepArgs& a, const float* __re
         nyD = a.nsq[HW + hD];
     }
     // own pixel
-    const float ax = (x - xl) + ux0, ay = (x - xu) + uy0;
-    const float zx = shrink_z<ISO>(ax, tau, nx0), zy = shrink_z<ISO>(ay, tau, ny0);
-    const float nux = ax - zx, nuy = ay - zy;
-    const float wx = zx - nux, wy = zy - nuy;
+    const T ax = (x - xl) + ux0, ay = (x - xu) + uy0;
+    const T zx = shrink_z<ISO>(ax, tau, nx0), zy = shrink_z<ISO>(ay, tau, ny0);
+    const T nux = ax - zx, nuy = ay - zy;
+    const T wx = zx - nux, wy = zy - nuy;
     // right neighbour's w_x and lower neighbour's w_y
-    const float axR = (xr - x) + uxR, ayD = (xd - x) + uyD;
-    const float zxR = shrink_z<ISO>(axR, tau, nxR), zyD = shrink_z<ISO>(ayD, tau, nyD);
-    const float wxR = zxR - (axR - zxR), wyD = zyD - (ayD - zyD);
+    const T axR = (xr - x) + uxR, ayD = (xd - x) + uyD;
+    const T zxR = shrink_z<ISO>(axR, tau, nxR), zyD = shrink_z<ISO>(ayD, tau, nyD);
+    const T wxR = zxR - (axR - zxR), wyD = zyD - (ayD - zyD);
     uxd[P0] = HIST ? ax : nux;
     uyd[P0] = HIST ? ay : nuy;
-    const float v = (wx - wxR) + (wy - wyD);
-    return fmaf(rho, v, bs[P0]);
+    const T v = (wx - wxR) + (wy - wyD);
+    return fmat(rho, v, bs[P0]);
 }
 
-template <bool ISO, bool FIRST, bool HIST>
-__device__ __forceinline__ float gstep_px(const GStepArgs& a, unsigned row, int j) {
+template <bool ISO, bool FIRST, bool HIST, class T>
+__device__ __forceinline__ T gstep_px(const GStepArgsT<T>& a, unsigned row, int j) {
     return gstep_pxr<ISO, FIRST, HIST>(a, a.x, a.b, a.uxi, a.uyi, a.uxo, a.uyo, row, j);
 }
 
-template <bool ISO, bool FIRST, bool HIST>
-__global__ void __launch_bounds__(256) k_gstep(GStepArgs a) {
+template <bool ISO, bool FIRST, bool HIST, class T = float>
+__global__ void __launch_bounds__(256) k_gstep(GStepArgsT<T> a) {
     // grid (rows P H, column chunks): one 32-bit division per thread instead of 64-bit ones
     const int j = (int)(blockIdx.y * blockDim.x + threadIdx.x);
     if (j >= a.W) return;
-    const float r = gstep_px<ISO, FIRST, HIST>(a, blockIdx.x, j);
+    const T r = gstep_px<ISO, FIRST, HIST>(a, blockIdx.x, j);
     if (a.r) a.r[(size_t)blockIdx.x * a.W + j] = r;
 }
 
 // the step fused into the next row transform (inference): a block computes r_{k+1} for its
 // 2 lines rows pixel by pixel (gstep_px, writing u_k) straight into the LDS image of k_grow_fwd,
 // so r never goes through HBM (-8 B/px and one launch per iteration)
-template <int BM, bool TWG, bool ISO, bool FIRST, int NT = GNT>
-__global__ void __launch_bounds__(NT) k_grow_fwd_step(GRowArgs a, GStepArgs g) {
+template <int BM, bool TWG, bool ISO, bool FIRST, int NT = GNT, class T = float>
+__global__ void __launch_bounds__(NT) k_grow_fwd_step(GRowArgsT<T> a, GStepArgsT<T> g) {
+    using C = cx_t<T>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
-    cf* twl = reinterpret_cast<cf*>(smem);
-    cf* A = twl + (TWG ? 0 : W + a.plan.ntab);
-    cf* B = A + (size_t)W * lines;
-    cf* X = B + (size_t)W * lines;
+    C* twl = reinterpret_cast<C*>(smem);
+    C* A = twl + (TWG ? 0 : W + a.plan.ntab);
+    C* B = A + (size_t)W * lines;
+    C* X = B + (size_t)W * lines;
     if constexpr (!TWG)
         for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
-    const cf* tw = TWG ? a.tw : twl;
+    const C* tw = TWG ? a.tw : twl;
     const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);
     // both rows of a complex line per step: two pixels' loads in flight together
     for (int c = 0; c < lines; ++c)
         for (int i = threadIdx.x; i < W; i += blockDim.x) {
             const int rr = 2 * c;
-            float v0 = 0.f, v1 = 0.f;
+            T v0 = 0, v1 = 0;
             if (rr + 1 < nl) {
                 v0 = gstep_pxr<ISO, FIRST, false>(g, g.x, g.b, g.uxi, g.uyi, g.uxo, g.uyo, (unsigned)(r0 + rr), i);
                 v1 = gstep_pxr<ISO, FIRST, false>(g, g.x, g.b, g.uxi, g.uyi, g.uxo, g.uyo, (unsigned)(r0 + rr + 1), i);
             } else if (rr < nl) {
                 v0 = gstep_pxr<ISO, FIRST, false>(g, g.x, g.b, g.uxi, g.uyi, g.uxo, g.uyo, (unsigned)(r0 + rr), i);
             }
-            A[i * lines + c] = mkc(v0, v1);  // even row -> real part, odd row -> imaginary part
+            A[i * lines + c] = mkx<T>(v0, v1);  // even row -> real part, odd row -> imaginary part
         }
     __syncthreads();
-    const cf* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
+    const C* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
+    const T half = T(0.5);
     for (int c = 0; c < lines; ++c)
         for (int k = threadIdx.x; k < Wh; k += blockDim.x) {
-            const cf z = res[k * lines + c];
-            const cf m = res[(k == 0 ? 0 : W - k) * lines + c];
+            const C z = res[k * lines + c];
+            const C m = res[(k == 0 ? 0 : W - k) * lines + c];
             const long long ra = r0 + 2 * c;
-            if (2 * c < nl) a.spec[ra * Wh + k] = mkc(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));
-            if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkc(0.5f * (z.y + m.y), 0.5f * (m.x - z.x));
+            if (2 * c < nl) a.spec[ra * Wh + k] = mkx<T>(half * (z.x + m.x), half * (z.y - m.y));
+            if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkx<T>(half * (z.y + m.y), half * (m.x - z.x));
         }
 }
 
 // iso: N_k[pixel] = sum over planes of a_x^2, a_y^2 with a = D x_k + u_{k-1}
-template <bool FIRST, bool HIST>
-__global__ void __launch_bounds__(256) k_giso_norm(const float* __restrict__ x, const float* __restrict__ uxi,
-                                                   const float* __restrict__ uyi, const float* __restrict__ nprev,
-                                                   const float* __restrict__ lam, const float* __restrict__ rho,
-                                                   float* __restrict__ nsq, int H, int W, long long P) {
+template <bool FIRST, bool HIST, class T = float>
+__global__ void __launch_bounds__(256) k_giso_norm(const T* __restrict__ x, const T* __restrict__ uxi,
+                                                   const T* __restrict__ uyi, const T* __restrict__ nprev,
+                                                   const T* __restrict__ lam, const T* __restrict__ rho,
+                                                   T* __restrict__ nsq, int H, int W, long long P) {
     const long long HW = (long long)H * W;
     const long long hw = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (hw >= HW) return;
     const int i = (int)(hw / W), j = (int)(hw % W);
     const int jm = j == 0 ? W - 1 : j - 1, im = i == 0 ? H - 1 : i - 1;
-    const float tau = lam[0] / rho[0];
-    float sx = 0.f, sy = 0.f;
+    const T tau = lam[0] / rho[0];
+    T sx = 0, sy = 0;
     for (long long p = 0; p < P; ++p) {
         const long long o = p * HW;
-        const float xc = x[o + hw];
-        const float ux = gprev_u<true, FIRST, HIST>(uxi, nprev, (size_t)(o + hw), (size_t)hw, tau);
-        const float uy = gprev_u<true, FIRST, HIST>(uyi, nprev ? nprev + HW : nullptr, (size_t)(o + hw), (size_t)hw, tau);
-        const float ax = (xc - x[o + (long long)i * W + jm]) + ux;
-        const float ay = (xc - x[o + (long long)im * W + j]) + uy;
-        sx = fmaf(ax, ax, sx);
-        sy = fmaf(ay, ay, sy);
+        const T xc = x[o + hw];
+        const T ux = gprev_u<true, FIRST, HIST>(uxi, nprev, (size_t)(o + hw), (size_t)hw, tau);
+        const T uy = gprev_u<true, FIRST, HIST>(uyi, nprev ? nprev + HW : nullptr, (size_t)(o + hw), (size_t)hw, tau);
+        const T ax = (xc - x[o + (long long)i * W + jm]) + ux;
+        const T ay = (xc - x[o + (long long)im * W + j]) + uy;
+        sx = fmat(ax, ax, sx);
+        sy = fmat(ay, ay, sy);
     }
     nsq[hw] = sx;
     nsq[HW + hw] = sy;
@@ -759,39 +784,40 @@ __global__ void __launch_bounds__(256) k_giso_norm(const float* __restrict__ x, 
 // ---------------------------------------------------------------------------
 // backward: per-pixel reverse step (the generic k_bwd_pass_a)
 // ---------------------------------------------------------------------------
-struct GBwdArgs {
-    const float* rb;      // r^_k                               [P][H][W]
-    float* xb;            // x^_{k-1} (k >= 2)
-    float* bbar;          // b^ accumulator
-    const float* abx_in;  // a^_k (k < K)
-    const float* aby_in;
-    float* abx_out;       // a^_{k-1} (k >= 2)
-    float* aby_out;
-    const float* akx;     // a_k
-    const float* aky;
-    const float* apx;     // a_{k-1} (k >= 2)
-    const float* apy;
-    const float* np;      // iso: N_{k-1}  [2][H][W]
-    const float* qp;      // iso: Q_{k-1}  [2][H][W]
-    const float* lam;
-    const float* rho;
-    float* part;          // per block {rho^, tau^}
+template <class T> struct GBwdArgsT {
+    const T* rb;          // r^_k                               [P][H][W]
+    T* xb;                // x^_{k-1} (k >= 2)
+    T* bbar;              // b^ accumulator
+    const T* abx_in;      // a^_k (k < K)
+    const T* aby_in;
+    T* abx_out;           // a^_{k-1} (k >= 2)
+    T* aby_out;
+    const T* akx;         // a_k
+    const T* aky;
+    const T* apx;         // a_{k-1} (k >= 2)
+    const T* apy;
+    const T* np;          // iso: N_{k-1}  [2][H][W]
+    const T* qp;          // iso: Q_{k-1}  [2][H][W]
+    const T* lam;
+    const T* rho;
+    T* part;              // per block {rho^, tau^}
     int H, W;
     long long npx;
 };
+using GBwdArgs = GBwdArgsT<float>;
 
-template <bool ISO, bool LASTK, bool FIRSTK>
-__device__ __forceinline__ float gabar(float d, float ap, float ub, float tau, float rho, float n, float q) {
-    const float wb = rho * d;
-    const float zb = 2.f * wb - ub;
+template <bool ISO, bool LASTK, bool FIRSTK, class T>
+__device__ __forceinline__ T gabar(T d, T ap, T ub, T tau, T rho, T n, T q) {
+    const T wb = rho * d;
+    const T zb = T(2) * wb - ub;
     return ub - wb + shrink_vjp<ISO>(ap, zb, tau, n, q);
 }
 
-template <bool ISO, bool LASTK, bool FIRSTK>
-__global__ void __launch_bounds__(256) k_gbwd(GBwdArgs a) {
-    __shared__ float red[2][256];
+template <bool ISO, bool LASTK, bool FIRSTK, class T = float>
+__global__ void __launch_bounds__(256) k_gbwd(GBwdArgsT<T> a) {
+    __shared__ T red[2][256];
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    float rho_acc = 0.f, tau_acc = 0.f;
+    T rho_acc = 0, tau_acc = 0;
     if (idx < a.npx) {
         const int H = a.H, W = a.W;
         const long long HW = (long long)H * W;
@@ -801,14 +827,14 @@ __global__ void __launch_bounds__(256) k_gbwd(GBwdArgs a) {
         const int im = i == 0 ? H - 1 : i - 1, ip = i == H - 1 ? 0 : i + 1;
         const size_t P0 = (size_t)idx, PR = (size_t)(pb + (long long)i * W + jp), PD = (size_t)(pb + (long long)ip * W + j);
         const size_t h0 = (size_t)rem, hR = (size_t)i * W + jp, hD = (size_t)ip * W + j;
-        const float rho = a.rho[0];
-        const float tau = a.lam[0] / rho;
-        const float r0 = a.rb[P0];
-        const float rl = a.rb[pb + (long long)i * W + jm], rr = a.rb[PR];
-        const float ru = a.rb[pb + (long long)im * W + j], rd = a.rb[PD];
-        const float dx0 = r0 - rl, dy0 = r0 - ru;  // D r^ at the pixel
+        const T rho = a.rho[0];
+        const T tau = a.lam[0] / rho;
+        const T r0 = a.rb[P0];
+        const T rl = a.rb[pb + (long long)i * W + jm], rr = a.rb[PR];
+        const T ru = a.rb[pb + (long long)im * W + j], rd = a.rb[PD];
+        const T dx0 = r0 - rl, dy0 = r0 - ru;  // D r^ at the pixel
         // rho^ partial: D r^ . (w_{k-1} - D x_k), w = 2z - a, D x_k = a_k - a_{k-1} + z_{k-1}
-        float apx0 = 0.f, apy0 = 0.f, nx0 = 0.f, ny0 = 0.f;
+        T apx0 = 0, apy0 = 0, nx0 = 0, ny0 = 0;
         if constexpr (!FIRSTK) {
             apx0 = a.apx[P0];
             apy0 = a.apy[P0];
@@ -817,17 +843,17 @@ __global__ void __launch_bounds__(256) k_gbwd(GBwdArgs a) {
                 ny0 = a.np[HW + h0];
             }
         }
-        const float zpx = FIRSTK ? 0.f : shrink_z<ISO>(apx0, tau, nx0);
-        const float zpy = FIRSTK ? 0.f : shrink_z<ISO>(apy0, tau, ny0);
+        const T zpx = FIRSTK ? T(0) : shrink_z<ISO>(apx0, tau, nx0);
+        const T zpy = FIRSTK ? T(0) : shrink_z<ISO>(apy0, tau, ny0);
         {
-            const float ex = (2.f * zpx - apx0) - (a.akx[P0] - apx0 + zpx);
-            const float ey = (2.f * zpy - apy0) - (a.aky[P0] - apy0 + zpy);
-            rho_acc = fmaf(dx0, ex, dy0 * ey);
+            const T ex = (T(2) * zpx - apx0) - (a.akx[P0] - apx0 + zpx);
+            const T ey = (T(2) * zpy - apy0) - (a.aky[P0] - apy0 + zpy);
+            rho_acc = fmat(dx0, ex, dy0 * ey);
         }
         // b^ += r^
         a.bbar[P0] = LASTK ? r0 : a.bbar[P0] + r0;
         if constexpr (!FIRSTK) {
-            float qx0 = 0.f, qy0 = 0.f, qxR = 0.f, qyD = 0.f, nxR = 0.f, nyD = 0.f;
+            T qx0 = 0, qy0 = 0, qxR = 0, qyD = 0, nxR = 0, nyD = 0;
             if constexpr (ISO) {
                 qx0 = a.qp[h0];
                 qy0 = a.qp[HW + h0];
@@ -836,19 +862,19 @@ __global__ void __launch_bounds__(256) k_gbwd(GBwdArgs a) {
                 nxR = a.np[hR];
                 nyD = a.np[HW + hD];
             }
-            const float ubx0 = LASTK ? 0.f : a.abx_in[P0], uby0 = LASTK ? 0.f : a.aby_in[P0];
-            const float ubxR = LASTK ? 0.f : a.abx_in[PR], ubyD = LASTK ? 0.f : a.aby_in[PD];
-            const float abx0 = gabar<ISO, LASTK, FIRSTK>(dx0, apx0, ubx0, tau, rho, nx0, qx0);
-            const float aby0 = gabar<ISO, LASTK, FIRSTK>(dy0, apy0, uby0, tau, rho, ny0, qy0);
+            const T ubx0 = LASTK ? T(0) : a.abx_in[P0], uby0 = LASTK ? T(0) : a.aby_in[P0];
+            const T ubxR = LASTK ? T(0) : a.abx_in[PR], ubyD = LASTK ? T(0) : a.aby_in[PD];
+            const T abx0 = gabar<ISO, LASTK, FIRSTK>(dx0, apx0, ubx0, tau, rho, nx0, qx0);
+            const T aby0 = gabar<ISO, LASTK, FIRSTK>(dy0, apy0, uby0, tau, rho, ny0, qy0);
             // a^_x at the right neighbour, a^_y at the lower one
-            const float abxR = gabar<ISO, LASTK, FIRSTK>(rr - r0, a.apx[PR], ubxR, tau, rho, nxR, qxR);
-            const float abyD = gabar<ISO, LASTK, FIRSTK>(rd - r0, a.apy[PD], ubyD, tau, rho, nyD, qyD);
+            const T abxR = gabar<ISO, LASTK, FIRSTK>(rr - r0, a.apx[PR], ubxR, tau, rho, nxR, qxR);
+            const T abyD = gabar<ISO, LASTK, FIRSTK>(rd - r0, a.apy[PD], ubyD, tau, rho, nyD, qyD);
             a.abx_out[P0] = abx0;
             a.aby_out[P0] = aby0;
             a.xb[P0] = (abx0 - abxR) + (aby0 - abyD);
             if constexpr (!ISO) {
-                const float wbx = rho * dx0, wby = rho * dy0;
-                tau_acc = soft_dtau(apx0, 2.f * wbx - ubx0, tau) + soft_dtau(apy0, 2.f * wby - uby0, tau);
+                const T wbx = rho * dx0, wby = rho * dy0;
+                tau_acc = soft_dtau(apx0, T(2) * wbx - ubx0, tau) + soft_dtau(apy0, T(2) * wby - uby0, tau);
             }
         }
     }
@@ -869,25 +895,25 @@ __global__ void __launch_bounds__(256) k_gbwd(GBwdArgs a) {
 }
 
 // iso backward: Q_{k-1}[pixel] = sum over planes of a_{k-1} z^_{k-1}, z^ = 2 rho D r^_k - a^_k
-template <bool LASTK>
-__global__ void __launch_bounds__(256) k_giso_q(const float* __restrict__ rb, const float* __restrict__ abx,
-                                                const float* __restrict__ aby, const float* __restrict__ apx,
-                                                const float* __restrict__ apy, const float* __restrict__ rho_p,
-                                                float* __restrict__ q, int H, int W, long long P) {
+template <bool LASTK, class T = float>
+__global__ void __launch_bounds__(256) k_giso_q(const T* __restrict__ rb, const T* __restrict__ abx,
+                                                const T* __restrict__ aby, const T* __restrict__ apx,
+                                                const T* __restrict__ apy, const T* __restrict__ rho_p,
+                                                T* __restrict__ q, int H, int W, long long P) {
     const long long HW = (long long)H * W;
     const long long hw = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (hw >= HW) return;
     const int i = (int)(hw / W), j = (int)(hw % W);
     const int jm = j == 0 ? W - 1 : j - 1, im = i == 0 ? H - 1 : i - 1;
-    const float rho = rho_p[0];
-    float qx = 0.f, qy = 0.f;
+    const T rho = rho_p[0];
+    T qx = 0, qy = 0;
     for (long long p = 0; p < P; ++p) {
         const long long o = p * HW;
-        const float r0 = rb[o + hw];
-        const float zx = 2.f * rho * (r0 - rb[o + (long long)i * W + jm]) - (LASTK ? 0.f : abx[o + hw]);
-        const float zy = 2.f * rho * (r0 - rb[o + (long long)im * W + j]) - (LASTK ? 0.f : aby[o + hw]);
-        qx = fmaf(apx[o + hw], zx, qx);
-        qy = fmaf(apy[o + hw], zy, qy);
+        const T r0 = rb[o + hw];
+        const T zx = T(2) * rho * (r0 - rb[o + (long long)i * W + jm]) - (LASTK ? T(0) : abx[o + hw]);
+        const T zy = T(2) * rho * (r0 - rb[o + (long long)im * W + j]) - (LASTK ? T(0) : aby[o + hw]);
+        qx = fmat(apx[o + hw], zx, qx);
+        qy = fmat(apy[o + hw], zy, qy);
     }
     q[hw] = qx;
     q[HW + hw] = qy;
@@ -896,15 +922,16 @@ __global__ void __launch_bounds__(256) k_giso_q(const float* __restrict__ rb, co
 // PSF gradient on the generic path: acc[kx][ky] += sum_p conj(U_p) V_p at every half-plane
 // frequency, U, V 2-D spectra [P][H][Wh] (column-pass dumps).  With fcT: only
 // fc^2 Re(conj(U) V) is kept (the Wiener-factor path); without: the complex sum (Z).
-__global__ void k_gxspec_acc(const cf* __restrict__ U, const cf* __restrict__ V, long long P, int H, int Wh,
-                             const float* __restrict__ fcT, double2* __restrict__ acc) {
+template <class T = float>
+__global__ void k_gxspec_acc(const cx_t<T>* __restrict__ U, const cx_t<T>* __restrict__ V, long long P, int H,
+                             int Wh, const T* __restrict__ fcT, double2* __restrict__ acc) {
     const long long nf = (long long)H * Wh;
     const long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nf) return;
     const int ky = (int)(f / Wh), kx = (int)(f % Wh);
     double re = 0.0, im = 0.0;
     for (long long p = 0; p < P; ++p) {
-        const cf u = U[p * nf + f], v = V[p * nf + f];
+        const cx_t<T> u = U[p * nf + f], v = V[p * nf + f];
         re += (double)u.x * v.x + (double)u.y * v.y;
         im += (double)u.x * v.y - (double)u.y * v.x;
     }
