@@ -100,14 +100,15 @@ int admm_tv_abi_version(void);
 const char* admm_tv_build_hash(void);
 
 /* 1: (H, W) runs on the fused power-of-two kernels (H in [16,4096], W in [16,2048]);
- * 2: any other size whose lines fit the generic kernels' LDS image (two buffers of a line of
- *    n complex values: n up to 10,240), run on the generic kernels (mixed-radix
- *    transforms, per-pixel step; the reference accepts any size, deconv.py:103-106);
+ * 2: any other size up to 65,536 points per side, run on the generic kernels (mixed-radix
+ *    transforms, per-pixel step; the reference accepts any size, deconv.py:103-106): lines up to
+ *    10,240 points transform in the kernels' LDS image, longer ones in a global scratch slot per
+ *    block (part of the workspace);
  * 0: unsupported. */
 int admm_tv_supported(int64_t H, int64_t W);
 
-/* 1 when an fp64 solve (ADMM_TV_FLAG_F64) of (H, W) is supported: every line of each dimension fits
- * the double kernels' LDS image (up to 10,240 points; 0 otherwise). */
+/* 1 when an fp64 solve (ADMM_TV_FLAG_F64) of (H, W) is supported (up to 65,536 points per side;
+ * lines beyond 5,120 points transform in global scratch), 0 otherwise. */
 int admm_tv_supported_f64(int64_t H, int64_t W);
 
 /* Workspace bytes needed by admm_tv_forward for `desc`. */

@@ -54,7 +54,7 @@ def test_host_entry_points():
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
     assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 4096), (8, 64), (1, 1), (481, 321))] == [generic] * 5
     assert [lib.admm_tv_supported(*hw) for hw in ((4097, 16), (5000, 33))] == [generic] * 2  # beyond 4096
-    assert [lib.admm_tv_supported(*hw) for hw in ((10241, 16), (16, 12288), (0, 16))] == [0] * 3
+    assert [lib.admm_tv_supported(*hw) for hw in ((65537, 16), (16, 70000), (0, 16))] == [0] * 3
     d = _native.desc(64, 3, 1024, 1024, 21, False, 50)
     ws = _native.workspace_size(d)
     img = 64 * 3 * 1024 * 1024 * 4
@@ -70,7 +70,8 @@ def test_host_entry_points_f64():
     lib = _native.load()
     assert [lib.admm_tv_supported_f64(*hw) for hw in ((1024, 1024), (15, 17), (1, 1), (481, 321), (256, 4096))] \
         == [1] * 5
-    assert [lib.admm_tv_supported_f64(*hw) for hw in ((10241, 16), (0, 16))] == [0] * 2
+    assert [lib.admm_tv_supported_f64(*hw) for hw in ((65537, 16), (0, 16))] == [0] * 2
+    assert lib.admm_tv_supported_f64(6000, 12000) == 1  # fp64 lines beyond 5,120 points: global buffers
     d32 = _native.desc(2, 3, 64, 96, 5, False, 10)
     d64 = _native.desc(2, 3, 64, 96, 5, False, 10, f64=True)
     assert d64.flags & _native.ADMM_TV_FLAG_F64
@@ -90,7 +91,7 @@ def test_host_entry_points_f64():
 
 @pytest.mark.parametrize("field,value,code", [
     ("kw", 5, -3),      # non-square PSF -> ADMM_TV_ENONSQUARE
-    ("H", 10241, -2),   # unsupported size (a line longer than the generic kernels' LDS image)
+    ("H", 65537, -2),   # unsupported size (a line longer than 65,536 points)
     ("maxit", -1, -1),  # invalid
     ("kh", 99, -3),
 ])
@@ -151,14 +152,21 @@ def test_library_built_from_this_tree():
 
 
 def test_supported_sizes():
-    """admm_tv_supported (host-only): power-of-two sizes on the fused kernels (1), any other size
-    whose lines fit the generic kernels' LDS image (2; twiddles move to global memory beyond ~6,800
-    points; up to 10,240 per side), else 0."""
+    """admm_tv_supported (host-only): power-of-two sizes on the fused kernels (1), any other size up
+    to 65,536 per side on the generic kernels (2; twiddles move to global memory beyond ~6,800
+    points, the line buffers too beyond 10,240), else 0."""
     from admmtor import _native
     L = _native.load()
     assert L.admm_tv_supported(1024, 1024) == 1 and L.admm_tv_supported(4096, 2048) == 1
     assert L.admm_tv_supported(15, 17) == 2 and L.admm_tv_supported(4096, 4096) == 2
     assert L.admm_tv_supported(6000, 4000) == 2 and L.admm_tv_supported(6800, 16) == 2
     assert L.admm_tv_supported(7680, 4320) == 2 and L.admm_tv_supported(8192, 8192) == 2  # global twiddles
-    assert L.admm_tv_supported(10240, 16) == 2 and L.admm_tv_supported(10241, 16) == 0
-    assert L.admm_tv_supported(0, 16) == 0
+    assert L.admm_tv_supported(10240, 16) == 2 and L.admm_tv_supported(10241, 16) == 2  # global line buffers
+    assert L.admm_tv_supported(1, 12000) == 2 and L.admm_tv_supported(65536, 3) == 2
+    assert L.admm_tv_supported(65537, 16) == 0 and L.admm_tv_supported(0, 16) == 0
+    # long lines' scratch slots are part of the workspace, bounded by the items of one launch
+    from admmtor import _native as nat
+    small = nat.workspace_size(nat.desc(1, 1, 1, 12000, 0, False, 5))
+    assert small < (16 << 20)  # one 12,000-point row: one slot, not 1,024
+    big = nat.workspace_size(nat.desc(2, 3, 12000, 12000, 0, False, 5))
+    assert big >= 7 * 2 * 3 * 12000 * 12000 * 4

@@ -113,9 +113,9 @@ def test_g7_edges(cuda_dev):
 
 
 def test_oversized_image_is_a_loud_gap(cuda_dev):
-    # every H, W up to 10,240 runs (odd and long lines: tests/test_gpu_generic.py); beyond, it raises
+    # every H, W up to 65,536 runs (odd and long lines: tests/test_gpu_generic.py); beyond, it raises
     with pytest.raises(NotImplementedError):
-        solve(np.zeros((1, 1, 4, 10300), np.float32), None, 0.01, 0.02, False, 2, cuda_dev)
+        solve(np.zeros((1, 1, 2, 65537), np.float32), None, 0.01, 0.02, False, 2, cuda_dev)
 
 
 @pytest.mark.parametrize("shape,psf,iso", [

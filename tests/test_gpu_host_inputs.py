@@ -4,10 +4,12 @@ The reference accepts tensors on any device and of any float dtype (deconv.py:35
 notebook calls it on CPU tensors (test_torch_admm.ipynb:249 ``fft_admm_tv(...)`` and :302
 ``ADMMDeconv((3,3),150,0.02,0.04,iso=False)(xin)``).  Here host tensors are staged to the ROCm
 device, solved by the HIP kernels and copied back (autograd through both copies); fp64 inputs
-compute in fp32 and return fp64.  Goldens: tests/golden/g10_notebook.npz, made by running the
-reference (tests/golden/make_golden_notebook.py).
+compute in fp64 (ADMM_TV_FLAG_F64) and return fp64.  Goldens: tests/golden/g10_notebook.npz, made by
+running the reference (tests/golden/make_golden_notebook.py).
 
-Gates: outputs <= 1e-5 relative L2 against the reference's fp64 result (BASELINE north star).
+Gates: fp32 outputs <= 1e-5 relative L2 against the reference's fp64 result (BASELINE north star);
+fp64 outputs 1e-6 (the goldens store the fp64 outputs and x gradients rounded to fp32; the fp64
+solve itself is pinned at 1e-12 in tests/test_gpu_f64.py).
 Gradients of the aniso module with a PSF pass near the soft threshold's kink (the
 reference's own fp32 gradients are 2.4e-3 (x) / 3.4e-4 (w) away from its fp64 ones, stored in the
 golden), so they are gated at 3x the reference's own fp32 distance plus 1e-4.
@@ -50,7 +52,7 @@ def test_notebook_cell15_cpu_tensors(cuda_dev, g10, dtype):
     _native_loaded()
     e = rel(r.numpy(), g10["nb249_ref64"])
     print(f"cell15 {dtype}: {e:.3e} (reference fp32: {float(g10['nb249_ref32_err']):.3e})")
-    assert e <= 1e-5
+    assert e <= (1e-6 if dtype == torch.float64 else 1e-5)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
@@ -73,19 +75,22 @@ def test_notebook_cell21_module_on_cpu(cuda_dev, g10, dtype):
     ew = rel(m.w.grad.numpy(), g10["nb302_gw64"])
     fx, fw = float(g10["nb302_gx_ref32_err"]), float(g10["nb302_gw_ref32_err"])
     print(f"cell21 {dtype}: out {e:.3e}, x.grad {ex:.3e} (ref fp32 {fx:.3e}), w.grad {ew:.3e} (ref fp32 {fw:.3e})")
-    assert e <= 1e-5
-    assert ex <= 3 * fx + 1e-4
-    assert ew <= 3 * fw + 1e-4
+    if dtype == torch.float64:  # fp64 solve: the reference's fp64 trajectory, no kink flips
+        assert e <= 1e-6 and ex <= 1e-5 and ew <= 1e-5
+    else:
+        assert e <= 1e-5
+        assert ex <= 3 * fx + 1e-4
+        assert ew <= 3 * fw + 1e-4
 
 
 def test_fp64_device_input_returns_fp64(cuda_dev, g10):
-    """fp64 tensors already on the device: computed in fp32, returned fp64 on the device."""
+    """fp64 tensors already on the device: computed in fp64, returned fp64 on the device."""
     from admmtor.eops.deconv import fft_admm_tv
     x = torch.from_numpy(g10["nb249_x"]).double().to(cuda_dev)
     k = torch.from_numpy(g10["nb249_k"]).double().to(cuda_dev)
     r = fft_admm_tv(x, 0.02, 0.02, k, True, 300)
     assert r.is_cuda and r.dtype == torch.float64
-    assert rel(r.cpu().numpy(), g10["nb249_ref64"]) <= 1e-5
+    assert rel(r.cpu().numpy(), g10["nb249_ref64"]) <= 1e-6
 
 
 def test_host_and_device_inputs_give_the_same_bits(cuda_dev, g10):

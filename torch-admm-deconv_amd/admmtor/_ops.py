@@ -51,7 +51,7 @@ def _check_supported(H: int, W: int, f64: bool) -> None:
     if not _native.supported(H, W, f64):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported"
                                   f"{'_f64' if f64 else ''}: any size whose lines fit the generic kernels' LDS, "
-                                  "up to 10,240)")
+                                  "up to 65,536)")
 
 
 def _flags(kern: Tensor, psf_grad: bool) -> int:

@@ -149,7 +149,7 @@ def _solve(x32: torch.Tensor, k32: torch.Tensor, lam: torch.Tensor, rho: torch.T
     d = _native.desc(B, C, H, W, k, iso, maxit, 0, G, bound, f64=f64)
     if not _native.supported(H, W, f64):
         raise NotImplementedError(f"admmtor (MI355X build): H={H}, W={W} unsupported (admm_tv_supported: any "
-                                  "size whose lines fit the generic kernels' LDS, up to 10,240)")
+                                  "size up to 65,536 per side)")
     ws = torch.empty(_native.workspace_size(d), dtype=torch.uint8, device=x32.device)
     bound.add(ws)
     out = torch.empty((G * B, C, H, W), dtype=x32.dtype, device=x32.device)

@@ -94,10 +94,11 @@ bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 bool supported_hw(int64_t H, int64_t W) {
     return pow2(H) && pow2(W) && H >= 16 && H <= 4096 && W >= 16 && W <= 2048;
 }
-// any other size runs on the generic kernels (generic_kernels.hpp), as long as one line of each
-// dimension fits their LDS image (two line buffers + twiddles and Bluestein tables, the latter read
-// from global memory for lines beyond ~6,800 points): up to 10,240
-constexpr int64_t kGenericMax = 10240;
+// any other size runs on the generic kernels (generic_kernels.hpp): a line of each dimension in
+// their LDS image (two line buffers + twiddles and Bluestein tables, the latter read from global
+// memory for lines beyond ~6,800 points) up to 10,240 points (5,120 in fp64); longer lines keep
+// their two buffers in a global scratch slot per block (GPlan::glb), up to kGenericMax
+constexpr int64_t kGenericMax = 65536;
 bool gen_fits(int n, bool f64 = false);  // below, with the plans
 bool generic_hw(int64_t H, int64_t W) {
     return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax && gen_fits((int)H) &&
@@ -115,6 +116,7 @@ int env_int(const char* name, int dflt) {
 }
 
 GPlan make_plan(int n, bool f64 = false);  // generic-size transform plan (below)
+size_t glb_scratch(int H, int W, long long P, bool f64);  // long lines' scratch bytes (below)
 
 // modules solved together (admm_tv_desc.groups)
 int ngroups_of(const admm_tv_desc& d) { return d.groups > 1 ? d.groups : 1; }
@@ -125,6 +127,7 @@ size_t up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 struct Layout {
     size_t spec[2], u[4], b, fcT, mT, twW, twH, twHd, G, part, nsq, sigma, total;
     size_t rimg;  // generic path: spec[0] = half spectra [P][H][W/2+1], spec[1] = x image, rimg = r image
+    size_t gscr;  // generic path, lines beyond the LDS image: the transform blocks' scratch slots
     int ngroups, ppg;
     bool gen;
 };
@@ -161,6 +164,7 @@ Layout make_layout(const admm_tv_desc& d) {
     L.twH = take((H + (L.gen ? make_plan((int)H, f64).ntab : 0)) * csz);
     L.twHd = take(H * sizeof(double2));
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
+    L.gscr = L.gen ? take(glb_scratch((int)H, (int)W, (long long)P, f64)) : 0;
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
         // plane groups for the iso norm pass: enough (group,row) items to fill the chip
@@ -463,7 +467,7 @@ int validate(const admm_tv_desc* d) {
         return fail(ADMM_TV_EINVAL, "invalid sizes or maxit");
     if (d->kh != d->kw) return fail(ADMM_TV_ENONSQUARE, "non-square PSF (the reference's H_t swaps H/W pads)");
     if (is_f64(*d) ? !f64_hw(d->H, d->W) : (!supported_hw(d->H, d->W) && !generic_hw(d->H, d->W)))
-        return fail(ADMM_TV_EUNSUPPORTED, "unsupported H, W (admm_tv_supported / admm_tv_supported_f64)");
+        return fail(ADMM_TV_EUNSUPPORTED, "unsupported H, W (admm_tv_supported / admm_tv_supported_f64: up to 65,536)");
     if (is_f64(*d) && d->groups > 1) return fail(ADMM_TV_EUNSUPPORTED, "groups > 1: fp32 only");
     if (d->kh > d->H || d->kw > d->W) return fail(ADMM_TV_EKERNEL, "PSF larger than the image");
     if (d->groups > 1 && (!supported_hw(d->H, d->W) || (d->flags & ADMM_TV_FLAG_PSF_GRAD)))
@@ -678,7 +682,16 @@ constexpr size_t kMaxLds = 160 * 1024;
 // LDS bytes of a generic transform kernel: twiddles + tables, two line buffers, Bluestein exchange
 // (csz: bytes of a complex element, 16 for the fp64 kernels)
 size_t glds(int n, int lines, const GPlan& p, size_t csz = sizeof(cf)) {
+    if (p.glb) return 0;  // the line buffers live in global scratch
     return csz * ((p.twg ? 0 : (size_t)n + p.ntab) + 2 * (size_t)n * lines + p.xslots);
+}
+
+// long-line blocks (GPlan::glb): scratch slots (resident blocks walking their items grid-stride) and
+// the bytes of the scratch region a solve needs for its longer dimension
+constexpr long long kGlbSlots = 1024;
+constexpr size_t kGlbBudget = 512ull << 20;
+long long glb_slots(int n, size_t csz) {
+    return std::max<long long>(64, std::min<long long>(kGlbSlots, (long long)(kGlbBudget / (2 * (size_t)n * csz))));
 }
 
 // fp64 plan: any prime > 5 first (its stage at NS = 1 needs no twiddle pass), then radices 4, 2, 3, 5
@@ -707,6 +720,7 @@ GPlan make_plan_f64(int n) {
     take_all(3);
     take_all(5);
     p.twg = glds(n, 1, p, sizeof(double2)) > kMaxLds ? 1 : 0;
+    p.glb = (p.twg && glds(n, 1, p, sizeof(double2)) > kMaxLds) ? 1 : 0;
     return p;
 }
 
@@ -733,15 +747,27 @@ GPlan make_plan(int n, bool f64) {
     p.bm = M;
     p.ntab = off - n;
     p.xslots = M > 0 ? (GNT / (M / blue_e(M))) * (M + M / 8) : 0;
-    // one line must fit the LDS: else no Bluestein, else twiddles from global memory
+    // one line must fit the LDS: else no Bluestein, else twiddles from global memory, else the
+    // line buffers too (a global scratch slot per block)
     if (glds(n, 1, p) <= kMaxLds) return p;
     GPlan q = make_plan_radices(n);
     q.twg = glds(n, 1, q) > kMaxLds ? 1 : 0;
+    if (q.twg && glds(n, 1, q) > kMaxLds) q.glb = 1;
     return q;
 }
 
 bool gen_fits(int n, bool f64) {
-    return glds(n, 1, make_plan(n, f64), f64 ? sizeof(double2) : sizeof(cf)) <= kMaxLds;
+    return n >= 1 && n <= kGenericMax && glds(n, 1, make_plan(n, f64), f64 ? sizeof(double2) : sizeof(cf)) <= kMaxLds;
+}
+// (as many slots as a launch of that dimension uses: min(slots, its items) -- gen_grid)
+size_t glb_scratch(int H, int W, long long P, bool f64) {
+    const size_t csz = f64 ? sizeof(double2) : sizeof(cf);
+    size_t b = 0;
+    if (make_plan(W, f64).glb)  // row transforms: two real rows per item
+        b = std::max(b, (size_t)std::min(glb_slots(W, csz), (P * H + 1) / 2) * 2 * (size_t)W * csz);
+    if (make_plan(H, f64).glb)  // column pass: one column per item
+        b = std::max(b, (size_t)std::min(glb_slots(H, csz), P * (W / 2 + 1)) * 2 * (size_t)H * csz);
+    return b;
 }
 
 // threads per block of the generic transform kernels (A/B knob; 64, 128 or 256)
@@ -760,9 +786,11 @@ bool gen_wide(int n, const GPlan& p) {
     return p.bm == 0 && mn > 0 && n >= mn;
 }
 
+// f(integral_constant BM, bool_constant TWG, bool_constant GLB)
 template <class F> int with_plan(const GPlan& p, F&& f) {
-    if (p.twg) return f(std::integral_constant<int, 0>{}, std::true_type{});
-    return with_bm(p.bm, [&](auto bm) { return f(bm, std::false_type{}); });
+    if (p.glb) return f(std::integral_constant<int, 0>{}, std::true_type{}, std::true_type{});
+    if (p.twg) return f(std::integral_constant<int, 0>{}, std::true_type{}, std::false_type{});
+    return with_bm(p.bm, [&](auto bm) { return f(bm, std::false_type{}, std::false_type{}); });
 }
 
 // the kernel instantiation for a plan's Bluestein size
@@ -846,11 +874,13 @@ int fit_lines(int n, int lines, const GPlan& p, size_t csz = sizeof(cf)) {
     return lines;
 }
 int grow_lines(int W, const GPlan& p, size_t csz = sizeof(cf)) {
+    if (p.glb) return 1;  // one line per scratch slot
     if (csz != sizeof(cf)) return fit_lines(W, pow2_floor(std::max(1, std::min(32, (2048 / W - 1) / 2))), p, csz);
     const int dflt = pow2_floor(std::max(1, std::min(32, (4096 / W - 1) / 2)));
     return fit_lines(W, pow2_floor(std::max(1, std::min(32, env_int("ADMM_GROW_LINES", dflt)))), p);
 }
 int gcol_cols(int H, const GPlan& p, size_t csz = sizeof(cf)) {
+    if (p.glb) return 1;
     if (csz != sizeof(cf)) return fit_lines(H, pow2_floor(std::max(1, std::min(16, (3072 / H - 1) / 2))), p, csz);
     // column blocks: ~48 KB LDS images without Bluestein stages (VGA 480: 2 -> 4 columns +7 %,
     // 500: +4 %, HD 1080: 1 -> 2 columns +6 %; tools/bench_generic_sizes.py), ~32 KB with them
@@ -875,119 +905,133 @@ template <class T> constexpr size_t kCsz = sizeof(cx_t<T>);
 template <class T, class F> int with_plan_t(const GPlan& p, F&& f) {
     if constexpr (kF64<T>) {
         if (p.bm != 0) return fail(ADMM_TV_EUNSUPPORTED, "fp64 plan with a Bluestein stage");
-        if (p.twg) return f(std::integral_constant<int, 0>{}, std::true_type{});
-        return f(std::integral_constant<int, 0>{}, std::false_type{});
+        if (p.glb) return f(std::integral_constant<int, 0>{}, std::true_type{}, std::true_type{});
+        if (p.twg) return f(std::integral_constant<int, 0>{}, std::true_type{}, std::false_type{});
+        return f(std::integral_constant<int, 0>{}, std::false_type{}, std::false_type{});
     } else {
         return with_plan(p, f);
     }
 }
+// grid of a transform launch: one block per item, or (long lines) the scratch slots walking them
+inline dim3 gen_grid(long long items, const GPlan& p, size_t csz) {
+    return dim3((unsigned)(p.glb ? std::min(items, glb_slots(p.n, csz)) : items));
+}
 
+#define GLB_CHECK(pl, gscr)                                                                          \
+    if ((pl).glb && !(gscr)) return fail(ADMM_TV_EINVAL, "long lines: no scratch region");
 template <class T>
-int grow_fwd(const T* img, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, hipStream_t s) {
+int grow_fwd(const T* img, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, hipStream_t s,
+             cx_t<T>* gscr = nullptr) {
     const GPlan pl = make_plan(W, kF64<T>);
-    GRowArgsT<T> a{img, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>)};
+    GLB_CHECK(pl, gscr)
+    GRowArgsT<T> a{img, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr};
     const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
-    return with_plan_t<T>(a.plan, [&](auto bm, auto twg) {
+    return with_plan_t<T>(a.plan, [&](auto bm, auto twg, auto glb) {
         constexpr int BM = decltype(bm)::value;
-        constexpr bool TWG = decltype(twg)::value;
-        const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
-        if constexpr (BM == 0 && !kF64<T>) {
+        constexpr bool TWG = decltype(twg)::value, GLB = decltype(glb)::value;
+        const dim3 grid = gen_grid((rows + 2 * a.lines - 1) / (2 * a.lines), pl, kCsz<T>);
+        if constexpr (BM == 0 && !kF64<T> && !GLB) {
             if (gen_wide(W, pl)) {
                 if (int e = set_lds(k_grow_fwd<BM, TWG, kGenWide>, lds)) return e;
                 hipLaunchKernelGGL((k_grow_fwd<BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
                 return launch_check("k_grow_fwd");
             }
         }
-        if (int e = set_lds(k_grow_fwd<BM, TWG, GNT, T>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_fwd<BM, TWG, GNT, T>), grid, dim3(kF64<T> ? GNT : gen_threads("ADMM_GROW_NT")), lds,
-                           s, a);
+        if (int e = set_lds(k_grow_fwd<BM, TWG, GNT, T, GLB>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_fwd<BM, TWG, GNT, T, GLB>), grid,
+                           dim3(kF64<T> || GLB ? GNT : gen_threads("ADMM_GROW_NT")), lds, s, a);
         return launch_check("k_grow_fwd");
     });
 }
 // the step fused into the row transform of r (k_grow_fwd_step; inference iterations)
 template <bool ISO, bool FIRST, class T>
-int grow_fwd_step_t(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, hipStream_t s) {
+int grow_fwd_step_t(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, hipStream_t s,
+                    cx_t<T>* gscr) {
     const GPlan pl = make_plan(W, kF64<T>);
-    GRowArgsT<T> a{nullptr, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>)};
+    GLB_CHECK(pl, gscr)
+    GRowArgsT<T> a{nullptr, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr};
     const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
-    return with_plan_t<T>(a.plan, [&](auto bm, auto twg) {
+    return with_plan_t<T>(a.plan, [&](auto bm, auto twg, auto glb) {
         constexpr int BM = decltype(bm)::value;
-        constexpr bool TWG = decltype(twg)::value;
-        const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
-        if constexpr (BM == 0 && !kF64<T>) {
+        constexpr bool TWG = decltype(twg)::value, GLB = decltype(glb)::value;
+        const dim3 grid = gen_grid((rows + 2 * a.lines - 1) / (2 * a.lines), pl, kCsz<T>);
+        if constexpr (BM == 0 && !kF64<T> && !GLB) {
             if (gen_wide(W, pl)) {
                 if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST, kGenWide>, lds)) return e;
                 hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST, kGenWide>), grid, dim3(kGenWide), lds, s, a, g);
                 return launch_check("k_grow_fwd_step");
             }
         }
-        if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST, GNT, T>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST, GNT, T>), grid,
-                           dim3(kF64<T> ? GNT : gen_threads("ADMM_GROW_NT")), lds, s, a, g);
+        if (int e = set_lds(k_grow_fwd_step<BM, TWG, ISO, FIRST, GNT, T, GLB>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_fwd_step<BM, TWG, ISO, FIRST, GNT, T, GLB>), grid,
+                           dim3(kF64<T> || GLB ? GNT : gen_threads("ADMM_GROW_NT")), lds, s, a, g);
         return launch_check("k_grow_fwd_step");
     });
 }
 template <class T>
 int grow_fwd_step(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, bool iso,
-                  bool first, hipStream_t s) {
-    if (iso) return first ? grow_fwd_step_t<true, true>(g, spec, tw, W, rows, s)
-                          : grow_fwd_step_t<true, false>(g, spec, tw, W, rows, s);
-    return first ? grow_fwd_step_t<false, true>(g, spec, tw, W, rows, s)
-                 : grow_fwd_step_t<false, false>(g, spec, tw, W, rows, s);
+                  bool first, hipStream_t s, cx_t<T>* gscr = nullptr) {
+    if (iso) return first ? grow_fwd_step_t<true, true>(g, spec, tw, W, rows, s, gscr)
+                          : grow_fwd_step_t<true, false>(g, spec, tw, W, rows, s, gscr);
+    return first ? grow_fwd_step_t<false, true>(g, spec, tw, W, rows, s, gscr)
+                 : grow_fwd_step_t<false, false>(g, spec, tw, W, rows, s, gscr);
 }
 template <class T>
-int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long rows, hipStream_t s) {
+int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long rows, hipStream_t s,
+             cx_t<T>* gscr = nullptr) {
     const GPlan pl = make_plan(W, kF64<T>);
-    GRowArgsT<T> a{nullptr, const_cast<cx_t<T>*>(spec), img, tw, pl, rows, grow_lines(W, pl, kCsz<T>)};
+    GLB_CHECK(pl, gscr)
+    GRowArgsT<T> a{nullptr, const_cast<cx_t<T>*>(spec), img, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr};
     const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
-    return with_plan_t<T>(a.plan, [&](auto bm, auto twg) {
+    return with_plan_t<T>(a.plan, [&](auto bm, auto twg, auto glb) {
         constexpr int BM = decltype(bm)::value;
-        constexpr bool TWG = decltype(twg)::value;
-        const dim3 grid((unsigned)((rows + 2 * a.lines - 1) / (2 * a.lines)));
-        if constexpr (BM == 0 && !kF64<T>) {
+        constexpr bool TWG = decltype(twg)::value, GLB = decltype(glb)::value;
+        const dim3 grid = gen_grid((rows + 2 * a.lines - 1) / (2 * a.lines), pl, kCsz<T>);
+        if constexpr (BM == 0 && !kF64<T> && !GLB) {
             if (gen_wide(W, pl)) {
                 if (int e = set_lds(k_grow_inv<BM, TWG, kGenWide>, lds)) return e;
                 hipLaunchKernelGGL((k_grow_inv<BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
                 return launch_check("k_grow_inv");
             }
         }
-        if (int e = set_lds(k_grow_inv<BM, TWG, GNT, T>, lds)) return e;
-        hipLaunchKernelGGL((k_grow_inv<BM, TWG, GNT, T>), grid, dim3(kF64<T> ? GNT : gen_threads("ADMM_GROW_NT")), lds,
-                           s, a);
+        if (int e = set_lds(k_grow_inv<BM, TWG, GNT, T, GLB>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_inv<BM, TWG, GNT, T, GLB>), grid,
+                           dim3(kF64<T> || GLB ? GNT : gen_threads("ADMM_GROW_NT")), lds, s, a);
         return launch_check("k_grow_inv");
     });
 }
-template <int MODE, int BM, bool TWG, class T>
+template <int MODE, int BM, bool TWG, bool GLB, class T>
 int gcol_launch(const GColArgsT<T>& a, size_t lds, dim3 grid, hipStream_t s) {
-    if constexpr (BM == 0 && !kF64<T>) {
+    if constexpr (BM == 0 && !kF64<T> && !GLB) {
         if (gen_wide(a.plan.n, a.plan)) {
             if (int e = set_lds(k_gcol<MODE, BM, TWG, kGenWide>, lds)) return e;
             hipLaunchKernelGGL((k_gcol<MODE, BM, TWG, kGenWide>), grid, dim3(kGenWide), lds, s, a);
             return launch_check("k_gcol");
         }
     }
-    if (int e = set_lds(k_gcol<MODE, BM, TWG, GNT, T>, lds)) return e;
-    hipLaunchKernelGGL((k_gcol<MODE, BM, TWG, GNT, T>), grid, dim3(kF64<T> ? GNT : gen_threads("ADMM_GCOL_NT")), lds,
-                       s, a);
+    if (int e = set_lds(k_gcol<MODE, BM, TWG, GNT, T, GLB>, lds)) return e;
+    hipLaunchKernelGGL((k_gcol<MODE, BM, TWG, GNT, T, GLB>), grid,
+                       dim3(kF64<T> || GLB ? GNT : gen_threads("ADMM_GCOL_NT")), lds, s, a);
     return launch_check("k_gcol");
 }
 template <class T>
 int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx_t<T>* tw, int H, int W, long long P,
-         int mode, hipStream_t s) {
+         int mode, hipStream_t s, cx_t<T>* gscr = nullptr) {
     const GPlan pl = make_plan(H, kF64<T>);
+    GLB_CHECK(pl, gscr)
     const int Wh = W / 2 + 1, cols = gcol_cols(H, pl, kCsz<T>);
     const int colblocks = (Wh + cols - 1) / cols;
-    GColArgsT<T> a{spec, dump, fcT, mT, tw, pl, Wh, cols, colblocks, P};
+    GColArgsT<T> a{spec, dump, fcT, mT, tw, pl, Wh, cols, colblocks, P, gscr};
     const size_t lds = glds(H, cols, a.plan, kCsz<T>);
-    const dim3 grid((unsigned)(P * colblocks));
-    return with_plan_t<T>(a.plan, [&](auto bm, auto twg) {
+    const dim3 grid = gen_grid(P * colblocks, pl, kCsz<T>);
+    return with_plan_t<T>(a.plan, [&](auto bm, auto twg, auto glb) {
         constexpr int BM = decltype(bm)::value;
-        constexpr bool TWG = decltype(twg)::value;
+        constexpr bool TWG = decltype(twg)::value, GLB = decltype(glb)::value;
         switch (mode) {
-            case 0: return gcol_launch<0, BM, TWG>(a, lds, grid, s);
-            case 1: return gcol_launch<1, BM, TWG>(a, lds, grid, s);
-            case 2: return gcol_launch<2, BM, TWG>(a, lds, grid, s);
-            default: return gcol_launch<3, BM, TWG>(a, lds, grid, s);
+            case 0: return gcol_launch<0, BM, TWG, GLB>(a, lds, grid, s);
+            case 1: return gcol_launch<1, BM, TWG, GLB>(a, lds, grid, s);
+            case 2: return gcol_launch<2, BM, TWG, GLB>(a, lds, grid, s);
+            default: return gcol_launch<3, BM, TWG, GLB>(a, lds, grid, s);
         }
     });
 }
@@ -999,10 +1043,11 @@ int gapply(const T* img_in, T* img_out, cx_t<T>* spec, const Layout& Lo, void* w
     const long long P = d.B * d.C, rows = P * d.H;
     const int H = (int)d.H, W = (int)d.W;
     C* twW = at<C>(ws, Lo.twW);
-    if (int e = grow_fwd(img_in, spec, twW, W, rows, s)) return e;
-    if (int e = gcol<T>(spec, nullptr, at<T>(ws, Lo.fcT), at<C>(ws, Lo.mT), at<C>(ws, Lo.twH), H, W, P, mode, s))
+    C* gs = at<C>(ws, Lo.gscr);
+    if (int e = grow_fwd(img_in, spec, twW, W, rows, s, gs)) return e;
+    if (int e = gcol<T>(spec, nullptr, at<T>(ws, Lo.fcT), at<C>(ws, Lo.mT), at<C>(ws, Lo.twH), H, W, P, mode, s, gs))
         return e;
-    return grow_inv<T>(spec, img_out, twW, W, rows, s);
+    return grow_inv<T>(spec, img_out, twW, W, rows, s, gs);
 }
 
 template <class T> int gstep(const GStepArgsT<T>& a, bool iso, bool first, bool hist, hipStream_t s) {
@@ -1079,6 +1124,7 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     T* fcT = at<T>(ws, Lo.fcT);
     C* mT = at<C>(ws, Lo.mT);
     C* spec = at<C>(ws, Lo.spec[0]);
+    C* gs = at<C>(ws, Lo.gscr);  // long lines: the transform blocks' scratch slots
     T* ximg = at<T>(ws, Lo.spec[1]);
     T* rimg = at<T>(ws, Lo.rimg);
     T* u[4] = {at<T>(ws, Lo.u[0]), at<T>(ws, Lo.u[1]), at<T>(ws, Lo.u[2]), at<T>(ws, Lo.u[3])};
@@ -1113,15 +1159,15 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     const long long crows = np * H;
     {
         ProfScope ps(3, st);
-        if (int e = grow_fwd(cb, cspec, twW, W, crows, st)) return e;  // r_1 = b
+        if (int e = grow_fwd(cb, cspec, twW, W, crows, st, gs)) return e;  // r_1 = b
     }
     int uin = 0;
     for (int it = 1; it <= d.maxit; ++it) {
         const bool last = it == d.maxit;
         {
             ProfScope ps(1, st);
-            if (int e = gcol<T>(cspec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, np, 0, st)) return e;
-            if (int e = grow_inv<T>(cspec, last ? cout : cx, twW, W, crows, st)) return e;
+            if (int e = gcol<T>(cspec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, np, 0, st, gs)) return e;
+            if (int e = grow_inv<T>(cspec, last ? cout : cx, twW, W, crows, st, gs)) return e;
         }
         if (last && !train) break;
         const T* xk = last ? cout : cx;
@@ -1161,11 +1207,11 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
             GStepArgsT<T> ga{xk, cb, uxi, uyi, uxo, uyo, last ? nullptr : crimg, nsq, nprev, lam, rho, H, W, np * H * W};
             // inference: the step runs inside the row transform of r (ADMM_GSTEP_FUSE=0: separate)
             if (!train && !last && env_int("ADMM_GSTEP_FUSE", 1)) {
-                if (int e = grow_fwd_step(ga, cspec, twW, W, crows, d.iso != 0, first, st)) return e;
+                if (int e = grow_fwd_step(ga, cspec, twW, W, crows, d.iso != 0, first, st, gs)) return e;
             } else {
                 if (int e = gstep(ga, d.iso != 0, first, train, st)) return e;
                 if (!last)
-                    if (int e = grow_fwd(crimg, cspec, twW, W, crows, st)) return e;
+                    if (int e = grow_fwd(crimg, cspec, twW, W, crows, st, gs)) return e;
             }
         }
         uin = 1 - uin;
@@ -1179,7 +1225,9 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cap));
     const long long h = gen_split(P, H);
-    if (!d.iso && !train && h > 0 && cap == hipStreamCaptureStatusNone && env_int("ADMM_GEN_STREAMS", 2) >= 2) {
+    // (long lines: the halves would share the transform blocks' scratch slots -- one stream)
+    const bool glb = make_plan(H, kF64<T>).glb || make_plan(W, kF64<T>).glb;
+    if (!d.iso && !train && h > 0 && !glb && cap == hipStreamCaptureStatusNone && env_int("ADMM_GEN_STREAMS", 2) >= 2) {
         int dev = 0;
         HIPCHK(hipGetDevice(&dev));
         hipStream_t s2 = aux_stream(s, dev);
@@ -1438,6 +1486,7 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, c
     }
     C* twW = at<C>(ws, Lo.twW);
     C* twH = at<C>(ws, Lo.twH);
+    C* gs = at<C>(ws, Lo.gscr);  // long lines: the transform blocks' scratch slots
     T* fcT = at<T>(ws, Lo.fcT);
     const long long rows = P * H;
     const dim3 fgrid((unsigned)((nf + 255) / 256)), fblk(256);
@@ -1459,9 +1508,9 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, c
             ProfScope ps(1, s);
             // r^_k = M x^_k; with the PSF gradient the column pass also dumps X^_k's spectrum and
             // A += fc^2 Re(sum_p conj(X^_k) R_k)
-            if (int e = grow_fwd(xbk, spec, twW, W, rows, s)) return e;
-            if (int e = gcol<T>(spec, xspec, fcT, at<C>(ws, Lo.mT), twH, H, W, P, 0, s)) return e;
-            if (int e = grow_inv<T>(spec, rb, twW, W, rows, s)) return e;
+            if (int e = grow_fwd(xbk, spec, twW, W, rows, s, gs)) return e;
+            if (int e = gcol<T>(spec, xspec, fcT, at<C>(ws, Lo.mT), twH, H, W, P, 0, s, gs)) return e;
+            if (int e = grow_inv<T>(spec, rb, twW, W, rows, s, gs)) return e;
             if (psf_grad) {
                 hipLaunchKernelGGL(k_gxspec_acc<T>, fgrid, fblk, 0, s, xspec, ht(k), P, H, Wh, fcT, at<double2>(ws, BL.aacc));
                 if (int e = launch_check("k_gxspec_acc")) return e;
@@ -1504,10 +1553,10 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, c
         return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
     }
     if (psf_grad) {  // Z = sum_p conj(Bbar_p) Xin_p, then the k x k taps
-        if (int e = grow_fwd(bbar, spec, twW, W, rows, s)) return e;
-        if (int e = gcol<T>(spec, xspec, nullptr, nullptr, twH, H, W, P, 3, s)) return e;
-        if (int e = grow_fwd(xin, spec, twW, W, rows, s)) return e;
-        if (int e = gcol<T>(spec, spec, nullptr, nullptr, twH, H, W, P, 3, s)) return e;
+        if (int e = grow_fwd(bbar, spec, twW, W, rows, s, gs)) return e;
+        if (int e = gcol<T>(spec, xspec, nullptr, nullptr, twH, H, W, P, 3, s, gs)) return e;
+        if (int e = grow_fwd(xin, spec, twW, W, rows, s, gs)) return e;
+        if (int e = gcol<T>(spec, spec, nullptr, nullptr, twH, H, W, P, 3, s, gs)) return e;
         hipLaunchKernelGGL(k_gxspec_acc<T>, fgrid, fblk, 0, s, xspec, spec, P, H, Wh, nullptr, at<double2>(ws, BL.zacc));
         if (int e = launch_check("k_gxspec_acc")) return e;
         hipLaunchKernelGGL(k_psf_grad<T>, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),

@@ -49,6 +49,9 @@ struct GPlan {
     int bm;            // the plan's Bluestein size M (all its Bluestein stages), 0: none
     int twg;           // 1: twiddles and tables are read from global memory (L1/L2), not LDS --
                        // long lines (> ~6,800 points) whose LDS image would not fit otherwise
+    int glb;           // 1: even the two line buffers do not fit the LDS (lines beyond 10,240 points,
+                       // 5,120 in fp64): they live in a global scratch slot per block (L2-resident),
+                       // blocks walk their lines grid-stride; implies twg, no Bluestein stages
 };
 
 // values per lane of the power-of-two transform of length M (fft_core.hpp RowCfg)
@@ -355,7 +358,7 @@ __device__ __forceinline__ void gstage_blue(const cf* __restrict__ src, cf* __re
 // BM: the plan's Bluestein size (a template parameter, so a kernel without Bluestein stages keeps
 // its small register footprint; each BM is its own kernel instantiation).
 template <int DIR, int BM, class C>
-__device__ C* gfft_lds(C* bufA, C* bufB, const GPlan& pl, int lines, const C* __restrict__ tw,
+__device__ __forceinline__ C* gfft_lds(C* bufA, C* bufB, const GPlan& pl, int lines, const C* __restrict__ tw,
                        C* __restrict__ xbuf) {  // bufA is clobbered
     static_assert(BM == 0 || std::is_same<C, cf>::value, "Bluestein stages: fp32 only");
     C* src = bufA;
@@ -455,7 +458,17 @@ template <class T> struct GRowArgsT {
     GPlan plan;
     long long rows;
     int lines;           // rows per block
+    cx_t<T>* gscr;       // plan.glb: the blocks' scratch slots, 2 W lines values each
 };
+
+// the line buffers of a transform block: the LDS image after the twiddles (twl), or -- long lines
+// (GLB) -- this block's slot of the global scratch.  Long-line blocks walk their work items
+// grid-stride (one scratch slot per block, ADMM_GEN_ITEMS), every other block runs its one item.
+template <bool GLB, class C>
+__device__ __forceinline__ C* line_bufs(C* twl, int tw_slots, C* gscr, size_t slot) {
+    if constexpr (GLB) return gscr + (size_t)blockIdx.x * slot;
+    else return twl + tw_slots;
+}
 using GRowArgs = GRowArgsT<float>;
 
 // Real rows are transformed two at a time: rows a, b as one complex row z = a + i b, whose
@@ -463,19 +476,11 @@ using GRowArgs = GRowArgsT<float>;
 // holds `lines` complex rows = 2 * lines real rows.
 // TWG: twiddles / tables read from global memory (GPlan::twg; a template parameter, so the LDS
 // variant keeps its LDS reads)
-template <int BM, bool TWG, int NT = GNT, class T = float>
-__global__ void __launch_bounds__(NT) k_grow_fwd(GRowArgsT<T> a) {
+template <int BM, class T>
+__device__ __forceinline__ void grow_fwd_item(const GRowArgsT<T>& a, cx_t<T>* A, cx_t<T>* B, cx_t<T>* X,
+                                              const cx_t<T>* tw, long long r0) {
     using C = cx_t<T>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
-    C* twl = reinterpret_cast<C*>(smem);
-    C* A = twl + (TWG ? 0 : W + a.plan.ntab);
-    C* B = A + (size_t)W * lines;
-    C* X = B + (size_t)W * lines;  // Bluestein exchange slots
-    if constexpr (!TWG)
-        for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
-    const C* tw = TWG ? a.tw : twl;
-    const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);  // real rows in this block
     for (int rr = 0; rr < 2 * lines; ++rr)  // coalesced along the row
         for (int i = threadIdx.x; i < W; i += blockDim.x) {
@@ -496,19 +501,39 @@ __global__ void __launch_bounds__(NT) k_grow_fwd(GRowArgsT<T> a) {
         }
 }
 
-template <int BM, bool TWG, int NT = GNT, class T = float>
-__global__ void __launch_bounds__(NT) k_grow_inv(GRowArgsT<T> a) {
+// GLB: long lines, the blocks' scratch slots walk the work items grid-stride (one slot per block)
+#define ADMM_GEN_ITEMS(nitems, stride, call)                                                        \
+    if constexpr (GLB) {                                                                            \
+        for (long long u_ = blockIdx.x; u_ < (nitems); u_ += gridDim.x) {                          \
+            call(u_ * (stride));                                                                    \
+            __syncthreads(); /* the slot's next item overwrites what this one still reads */       \
+        }                                                                                           \
+    } else {                                                                                        \
+        call((long long)blockIdx.x * (stride));                                                     \
+    }
+
+template <int BM, bool TWG, int NT = GNT, class T = float, bool GLB = false>
+__global__ void __launch_bounds__(NT) k_grow_fwd(GRowArgsT<T> a) {
     using C = cx_t<T>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
+    const int W = a.plan.n, lines = a.lines;
     C* twl = reinterpret_cast<C*>(smem);
-    C* A = twl + (TWG ? 0 : W + a.plan.ntab);
+    C* A = line_bufs<GLB>(twl, TWG ? 0 : W + a.plan.ntab, a.gscr, 2 * (size_t)W * lines);
     C* B = A + (size_t)W * lines;
-    C* X = B + (size_t)W * lines;
+    C* X = GLB ? nullptr : B + (size_t)W * lines;  // Bluestein exchange slots
     if constexpr (!TWG)
         for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
     const C* tw = TWG ? a.tw : twl;
-    const long long r0 = (long long)blockIdx.x * 2 * lines;
+#define ADMM_ITEM(r0) grow_fwd_item<BM>(a, A, B, X, tw, r0)
+    ADMM_GEN_ITEMS((a.rows + 2 * lines - 1) / (2 * lines), 2 * lines, ADMM_ITEM)
+#undef ADMM_ITEM
+}
+
+template <int BM, class T>
+__device__ __forceinline__ void grow_inv_item(const GRowArgsT<T>& a, cx_t<T>* A, cx_t<T>* B, cx_t<T>* X,
+                                              const cx_t<T>* tw, long long r0) {
+    using C = cx_t<T>;
+    const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);
     // Hermitian completion of a half spectrum: X[k] = conj X[W - k] for k >= Wh; the imaginary
     // parts of the self-conjugate bins (DC, and Nyquist for even W) are dropped, as irfft does
@@ -536,6 +561,23 @@ __global__ void __launch_bounds__(NT) k_grow_inv(GRowArgsT<T> a) {
         }
 }
 
+template <int BM, bool TWG, int NT = GNT, class T = float, bool GLB = false>
+__global__ void __launch_bounds__(NT) k_grow_inv(GRowArgsT<T> a) {
+    using C = cx_t<T>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int W = a.plan.n, lines = a.lines;
+    C* twl = reinterpret_cast<C*>(smem);
+    C* A = line_bufs<GLB>(twl, TWG ? 0 : W + a.plan.ntab, a.gscr, 2 * (size_t)W * lines);
+    C* B = A + (size_t)W * lines;
+    C* X = GLB ? nullptr : B + (size_t)W * lines;
+    if constexpr (!TWG)
+        for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
+    const C* tw = TWG ? a.tw : twl;
+#define ADMM_ITEM(r0) grow_inv_item<BM>(a, A, B, X, tw, r0)
+    ADMM_GEN_ITEMS((a.rows + 2 * lines - 1) / (2 * lines), 2 * lines, ADMM_ITEM)
+#undef ADMM_ITEM
+}
+
 // ---------------------------------------------------------------------------
 // column pass: per column kx of the half spectrum, FFT along H, multiply, inverse FFT.
 // MODE 0: real factor fcT[kx][ky]; 1: mT[kx][ky]; 2: conj(mT); 3: transform only (dump the
@@ -553,6 +595,7 @@ template <class T> struct GColArgsT {
     int cols;             // columns per block
     int colblocks;
     long long P;
+    cx_t<T>* gscr;        // plan.glb: the blocks' scratch slots, 2 H cols values each
 };
 using GColArgs = GColArgsT<float>;
 
@@ -563,21 +606,14 @@ using GColArgs = GColArgsT<float>;
 #endif
 constexpr int gcol_minw(int bm) { return bm == 256 ? ADMM_GCOL_MINW : 1; }
 
-template <int MODE, int BM, bool TWG, int NT = GNT, class T = float>
-__global__ void __launch_bounds__(NT, gcol_minw(BM)) k_gcol(GColArgsT<T> a) {
+template <int MODE, int BM, class T>
+__device__ __forceinline__ void gcol_item(const GColArgsT<T>& a, cx_t<T>* A, cx_t<T>* B, cx_t<T>* X,
+                                          const cx_t<T>* tw, long long item) {
     using C = cx_t<T>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.plan.n, Wh = a.Wh, cols = a.cols;
     const int lgc = __ffs(cols) - 1;  // cols is a power of two
-    C* twl = reinterpret_cast<C*>(smem);
-    C* A = twl + (TWG ? 0 : H + a.plan.ntab);
-    C* B = A + (size_t)H * cols;
-    C* X = B + (size_t)H * cols;
-    if constexpr (!TWG)
-        for (int i = threadIdx.x; i < H + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
-    const C* tw = TWG ? a.tw : twl;
-    const long long p = blockIdx.x / a.colblocks;
-    const int c0 = (int)(blockIdx.x % a.colblocks) * cols;
+    const long long p = item / a.colblocks;
+    const int c0 = (int)(item % a.colblocks) * cols;
     const int nc = min(cols, Wh - c0);
     C* S = a.spec + (size_t)p * H * Wh + c0;
     for (int idx = threadIdx.x; idx < H * cols; idx += blockDim.x) {
@@ -611,6 +647,23 @@ __global__ void __launch_bounds__(NT, gcol_minw(BM)) k_gcol(GColArgsT<T> a) {
         const int i = idx >> lgc, c = idx & (cols - 1);
         if (c < nc) S[(size_t)i * Wh + c] = out[i * cols + c];
     }
+}
+
+template <int MODE, int BM, bool TWG, int NT = GNT, class T = float, bool GLB = false>
+__global__ void __launch_bounds__(NT, gcol_minw(BM)) k_gcol(GColArgsT<T> a) {
+    using C = cx_t<T>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int H = a.plan.n, cols = a.cols;
+    C* twl = reinterpret_cast<C*>(smem);
+    C* A = line_bufs<GLB>(twl, TWG ? 0 : H + a.plan.ntab, a.gscr, 2 * (size_t)H * cols);
+    C* B = A + (size_t)H * cols;
+    C* X = GLB ? nullptr : B + (size_t)H * cols;
+    if constexpr (!TWG)
+        for (int i = threadIdx.x; i < H + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
+    const C* tw = TWG ? a.tw : twl;
+#define ADMM_ITEM(item) gcol_item<MODE, BM>(a, A, B, X, tw, item)
+    ADMM_GEN_ITEMS(a.P * a.colblocks, 1, ADMM_ITEM)
+#undef ADMM_ITEM
 }
 
 // ---------------------------------------------------------------------------
@@ -714,19 +767,11 @@ __global__ void __launch_bounds__(256) k_gstep(GStepArgsT<T> a) {
 // the step fused into the next row transform (inference): a block computes r_{k+1} for its
 // 2 lines rows pixel by pixel (gstep_px, writing u_k) straight into the LDS image of k_grow_fwd,
 // so r never goes through HBM (-8 B/px and one launch per iteration)
-template <int BM, bool TWG, bool ISO, bool FIRST, int NT = GNT, class T = float>
-__global__ void __launch_bounds__(NT) k_grow_fwd_step(GRowArgsT<T> a, GStepArgsT<T> g) {
+template <int BM, bool ISO, bool FIRST, class T>
+__device__ __forceinline__ void grow_fwd_step_item(const GRowArgsT<T>& a, const GStepArgsT<T>& g, cx_t<T>* A,
+                                                   cx_t<T>* B, cx_t<T>* X, const cx_t<T>* tw, long long r0) {
     using C = cx_t<T>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int W = a.plan.n, Wh = W / 2 + 1, lines = a.lines;
-    C* twl = reinterpret_cast<C*>(smem);
-    C* A = twl + (TWG ? 0 : W + a.plan.ntab);
-    C* B = A + (size_t)W * lines;
-    C* X = B + (size_t)W * lines;
-    if constexpr (!TWG)
-        for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
-    const C* tw = TWG ? a.tw : twl;
-    const long long r0 = (long long)blockIdx.x * 2 * lines;
     const int nl = (int)min((long long)2 * lines, a.rows - r0);
     // both rows of a complex line per step: two pixels' loads in flight together
     for (int c = 0; c < lines; ++c)
@@ -752,6 +797,23 @@ __global__ void __launch_bounds__(NT) k_grow_fwd_step(GRowArgsT<T> a, GStepArgsT
             if (2 * c < nl) a.spec[ra * Wh + k] = mkx<T>(half * (z.x + m.x), half * (z.y - m.y));
             if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkx<T>(half * (z.y + m.y), half * (m.x - z.x));
         }
+}
+
+template <int BM, bool TWG, bool ISO, bool FIRST, int NT = GNT, class T = float, bool GLB = false>
+__global__ void __launch_bounds__(NT) k_grow_fwd_step(GRowArgsT<T> a, GStepArgsT<T> g) {
+    using C = cx_t<T>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int W = a.plan.n, lines = a.lines;
+    C* twl = reinterpret_cast<C*>(smem);
+    C* A = line_bufs<GLB>(twl, TWG ? 0 : W + a.plan.ntab, a.gscr, 2 * (size_t)W * lines);
+    C* B = A + (size_t)W * lines;
+    C* X = GLB ? nullptr : B + (size_t)W * lines;
+    if constexpr (!TWG)
+        for (int i = threadIdx.x; i < W + a.plan.ntab; i += blockDim.x) twl[i] = a.tw[i];
+    const C* tw = TWG ? a.tw : twl;
+#define ADMM_ITEM(r0) grow_fwd_step_item<BM, ISO, FIRST>(a, g, A, B, X, tw, r0)
+    ADMM_GEN_ITEMS((a.rows + 2 * lines - 1) / (2 * lines), 2 * lines, ADMM_ITEM)
+#undef ADMM_ITEM
 }
 
 // iso: N_k[pixel] = sum over planes of a_x^2, a_y^2 with a = D x_k + u_{k-1}
