@@ -152,8 +152,10 @@ def test_two_stream_split_matches_one_stream(cuda_dev, monkeypatch, B, C, H, W):
     two = fft_admm_tv(x, 0.01, 0.02, k.to(cuda_dev), False, 8)
     monkeypatch.setenv("ADMM_GEN_STREAMS", "1")
     one = fft_admm_tv(x, 0.01, 0.02, k.to(cuda_dev), False, 8)
+    monkeypatch.setenv("ADMM_GEN_STREAMS", "4")
+    four = fft_admm_tv(x, 0.01, 0.02, k.to(cuda_dev), False, 8)
     torch.cuda.synchronize()
-    assert torch.equal(two, one)
+    assert torch.equal(two, one) and torch.equal(four, one)
 
 
 def test_input_on_another_device_than_current(cuda_dev):

@@ -579,8 +579,9 @@ struct DeviceGuard {
 // per-thread leak).  Bounded: beyond kAuxPerDev caller streams per device the entries are reused
 // round-robin (a reused entry only adds ordering, never a hazard).  The streams live until the
 // process ends (destroying them from a static destructor could race the HIP runtime's teardown).
+constexpr int kMaxAux = 3;  // auxiliary streams per caller stream (solves on up to 4 streams)
 struct AuxEntry {
-    hipStream_t caller = nullptr, aux = nullptr;
+    hipStream_t caller = nullptr, aux[kMaxAux] = {};
 };
 constexpr int kAuxDev = 64, kAuxPerDev = 32;
 struct AuxPool {
@@ -589,63 +590,74 @@ struct AuxPool {
     int used[kAuxDev] = {}, next[kAuxDev] = {};
 } g_aux;
 
-// the auxiliary stream paired with caller stream s on device dev (the current device, see DeviceGuard)
-hipStream_t aux_stream(hipStream_t s, int dev) {
-    if (dev < 0 || dev >= kAuxDev) return nullptr;
+// the k-th auxiliary stream (k < kMaxAux) paired with caller stream s on device dev (the current
+// device, see DeviceGuard), created on first use
+hipStream_t aux_stream(hipStream_t s, int dev, int k = 0) {
+    if (dev < 0 || dev >= kAuxDev || k < 0 || k >= kMaxAux) return nullptr;
     std::lock_guard<std::mutex> lk(g_aux.mu);
     AuxEntry* row = g_aux.e[dev];
-    for (int i = 0; i < g_aux.used[dev]; ++i)
-        if (row[i].caller == s) return row[i].aux;
-    AuxEntry* slot;
-    if (g_aux.used[dev] < kAuxPerDev) {
-        slot = &row[g_aux.used[dev]];
-        if (hipStreamCreateWithFlags(&slot->aux, hipStreamNonBlocking) != hipSuccess) {
-            slot->aux = nullptr;
-            return nullptr;
+    AuxEntry* slot = nullptr;
+    for (int i = 0; i < g_aux.used[dev] && !slot; ++i)
+        if (row[i].caller == s) slot = &row[i];
+    if (!slot) {
+        if (g_aux.used[dev] < kAuxPerDev) {
+            slot = &row[g_aux.used[dev]++];
+        } else {
+            slot = &row[g_aux.next[dev]];
+            g_aux.next[dev] = (g_aux.next[dev] + 1) % kAuxPerDev;
         }
-        ++g_aux.used[dev];
-    } else {
-        slot = &row[g_aux.next[dev]];
-        g_aux.next[dev] = (g_aux.next[dev] + 1) % kAuxPerDev;
+        slot->caller = s;
     }
-    slot->caller = s;
-    return slot->aux;
+    if (!slot->aux[k] && hipStreamCreateWithFlags(&slot->aux[k], hipStreamNonBlocking) != hipSuccess) {
+        slot->aux[k] = nullptr;
+        return nullptr;
+    }
+    return slot->aux[k];
 }
 
-// fork / join of a two-stream solve: s2 starts after the work already queued on s, and s waits
-// for everything queued on s2 -- also when a half fails after the fork (the join is always issued)
+// fork / join of a solve on several streams: the auxiliary streams start after the work already
+// queued on s, and s waits for everything queued on them -- also when a part fails after the fork
+// (every join is issued)
 struct ForkJoin {
-    hipStream_t s, s2;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t s;
+    std::vector<hipStream_t> aux;
+    hipEvent_t fork = nullptr;
+    std::vector<hipEvent_t> joins;
     hipError_t err = hipSuccess;
-    ForkJoin(hipStream_t a, hipStream_t b) : s(a), s2(b) {
+    ForkJoin(hipStream_t a, std::vector<hipStream_t> b) : s(a), aux(std::move(b)), joins(aux.size(), nullptr) {
         if ((err = hipEventCreateWithFlags(&fork, hipEventDisableTiming)) != hipSuccess) return;
-        if ((err = hipEventCreateWithFlags(&join, hipEventDisableTiming)) != hipSuccess) return;
+        for (auto& j : joins)
+            if ((err = hipEventCreateWithFlags(&j, hipEventDisableTiming)) != hipSuccess) return;
         if ((err = hipEventRecord(fork, s)) != hipSuccess) return;
-        err = hipStreamWaitEvent(s2, fork, 0);
+        for (hipStream_t x : aux)
+            if ((err = hipStreamWaitEvent(x, fork, 0)) != hipSuccess) return;
     }
     hipError_t finish() {
-        hipError_t e = hipEventRecord(join, s2);
-        if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
-        return e;
+        hipError_t first = hipSuccess;
+        for (size_t i = 0; i < aux.size(); ++i) {
+            hipError_t e = hipEventRecord(joins[i], aux[i]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, joins[i], 0);
+            if (first == hipSuccess) first = e;
+        }
+        return first;
     }
     ~ForkJoin() {
         if (fork) (void)hipEventDestroy(fork);
-        if (join) (void)hipEventDestroy(join);
+        for (hipEvent_t j : joins)
+            if (j) (void)hipEventDestroy(j);
     }
 };
 
-// split of P planes into two halves for the generic row kernels, which transform real rows in
-// pairs (rows 2c, 2c + 1 of a launch's range): the first half must hold an even number of rows,
-// or every pair of the second half would shift and the results would differ in the last bits
-// from a one-stream solve.  0: no split.
-long long gen_split(long long P, int H) {
-    long long h = P / 2;
-    if (H & 1) {
-        h &= ~1LL;
-        if (h == 0) h = P > 2 ? 2 : 0;
-    }
-    return (h > 0 && h < P) ? h : 0;
+// split of P planes into up to ns parts for the generic row kernels, which transform real rows in
+// pairs (rows 2c, 2c + 1 of a launch's range): every part but the last must hold an even number of
+// rows, or the pairs of the parts after it would shift and the results would differ in the last
+// bits from a one-stream solve.  Returns the parts' first planes (one entry: no split).
+std::vector<long long> gen_parts(long long P, int H, int ns) {
+    long long c = (P + ns - 1) / std::max(ns, 1);
+    if (H & 1) c += c & 1;  // an even plane count per part when H is odd
+    std::vector<long long> starts;
+    for (long long p = 0; p < P; p += std::max(c, 1LL)) starts.push_back(p);
+    return starts;
 }
 
 // planes per chunk of the aniso inference solve (run_forward): ADMM_CHUNK_PLANES > 0 sets it,
@@ -1218,24 +1230,32 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     }
     return 0;
     };
-    // two plane halves on two streams (the caller's and a per-thread auxiliary one): one half's
-    // compute-bound column pass overlaps the other half's row / step passes (ADMM_GEN_STREAMS,
+    // plane parts on several streams (the caller's and auxiliary ones, aux_stream): one part's
+    // compute-bound column pass overlaps another part's row / step passes (ADMM_GEN_STREAMS parts,
     // default 2: BSD 2,790 -> 3,150 it/s, every generic size measured gains).
     // Not under stream capture: a captured solve stays on the caller's stream.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cap));
-    const long long h = gen_split(P, H);
-    // (long lines: the halves would share the transform blocks' scratch slots -- one stream)
+    const int ns = std::max(1, std::min(kMaxAux + 1, env_int("ADMM_GEN_STREAMS", 2)));
+    const std::vector<long long> parts = gen_parts(P, H, ns);
+    // (long lines: the parts would share the transform blocks' scratch slots -- one stream)
     const bool glb = make_plan(H, kF64<T>).glb || make_plan(W, kF64<T>).glb;
-    if (!d.iso && !train && h > 0 && !glb && cap == hipStreamCaptureStatusNone && env_int("ADMM_GEN_STREAMS", 2) >= 2) {
+    if (!d.iso && !train && parts.size() > 1 && !glb && cap == hipStreamCaptureStatusNone) {
         int dev = 0;
         HIPCHK(hipGetDevice(&dev));
-        hipStream_t s2 = aux_stream(s, dev);
-        if (!s2) return fail(ADMM_TV_EHIP, "auxiliary stream");
-        ForkJoin fj(s, s2);
+        std::vector<hipStream_t> aux;
+        for (size_t i = 1; i < parts.size(); ++i) {
+            hipStream_t x = aux_stream(s, dev, (int)i - 1);
+            if (!x) return fail(ADMM_TV_EHIP, "auxiliary stream");
+            aux.push_back(x);
+        }
+        ForkJoin fj(s, aux);
         if (fj.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("fork: ") + hipGetErrorString(fj.err));
-        int e = solve_planes(0, h, s);
-        if (!e) e = solve_planes(h, P - h, s2);
+        int e = 0;
+        for (size_t i = 0; i < parts.size() && !e; ++i) {
+            const long long p1 = i + 1 < parts.size() ? parts[i + 1] : P;
+            e = solve_planes(parts[i], p1 - parts[i], i == 0 ? s : aux[i - 1]);
+        }
         const hipError_t je = fj.finish();
         if (e) return e;
         if (je != hipSuccess) return fail(ADMM_TV_EHIP, std::string("join: ") + hipGetErrorString(je));
@@ -1396,7 +1416,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         HIPCHK(hipGetDevice(&dev));
         hipStream_t s2 = aux_stream(s, dev);
         if (!s2) return fail(ADMM_TV_EHIP, "auxiliary stream");
-        ForkJoin fj(s, s2);
+        ForkJoin fj(s, {s2});
         if (fj.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("fork: ") + hipGetErrorString(fj.err));
         const long long h = P / 2;
         int e = solve_planes(0, h, h, s);
