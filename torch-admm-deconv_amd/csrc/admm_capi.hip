@@ -14,7 +14,7 @@
 #include <type_traits>
 #include <vector>
 
-#include "generic_kernels.hpp"
+#include "gcol_mm.hpp"
 #include "admm_tv.h"
 
 using namespace admm;
@@ -117,6 +117,14 @@ int env_int(const char* name, int dflt) {
 
 GPlan make_plan(int n, bool f64 = false);  // generic-size transform plan (below)
 size_t glb_scratch(int H, int W, long long P, bool f64);  // long lines' scratch bytes (below)
+// matrix-core column pass (gcol_mm.hpp): H = S R, odd R in [17, 127] carrying H's largest prime
+// factor (>= 17), S in {1, ..., 8} with a kernel instance; ok = false: the LDS column pass
+struct MMPlan {
+    bool ok;
+    int R, S, h, KS, MT, NL, RP;
+    size_t lds;
+};
+MMPlan mm_plan(int H, int W);
 
 // modules solved together (admm_tv_desc.groups)
 int ngroups_of(const admm_tv_desc& d) { return d.groups > 1 ? d.groups : 1; }
@@ -157,7 +165,8 @@ Layout make_layout(const admm_tv_desc& d) {
     L.b = (k > 0 || !L.gen) ? take(img_m) : 0;
     // one Wiener factor per module (its rho); on the fused path followed by their packed copies for
     // the column pass (k_fc_pack)
-    L.fcT = take(G * (N + 1) * H * rs * (L.gen ? 1 : 2));
+    // (generic path: a [H][Wh] copy for the matrix-core column pass, k_fc_transpose)
+    L.fcT = take(G * (N + 1) * H * rs * ((!L.gen || (!f64 && mm_plan((int)H, (int)W).ok)) ? 2 : 1));
     L.mT = take((N + 1) * H * csz);
     // twiddles; on the generic path followed by the plan's Bluestein tables (make_plan)
     L.twW = take((W + (L.gen ? make_plan((int)W, f64).ntab : 0)) * csz);
@@ -518,6 +527,12 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const T* kern, cons
                 hipLaunchKernelGGL(k_fc_pack, dim3((n + nt - 1) / nt), dim3(nt), 0, s, fc,
                                    fc + (size_t)ngroups_of(d) * n, H, N, col_e(H));
                 if (int e = launch_check("k_fc_pack")) return e;
+            }
+            if constexpr (std::is_same<T, float>::value) if (Lo.gen && mm_plan(H, W).ok) {
+                float* fc = at<float>(ws, Lo.fcT);  // the generic path has one module
+                hipLaunchKernelGGL(k_fc_transpose, dim3(std::min(4096, (n + nt - 1) / nt)), dim3(nt), 0, s, fc, fc + n, H,
+                                   N + 1);
+                if (int e = launch_check("k_fc_transpose")) return e;
             }
         }
     }
@@ -907,6 +922,46 @@ int gcol_cols(int H, const GPlan& p, size_t csz = sizeof(cf)) {
     return fit_lines(H, pow2_floor(std::max(1, std::min(32, env_int("ADMM_GCOL_COLS", dflt)))), p);
 }
 
+// matrix-core column pass plan (gcol_mm.hpp).  A/B knobs: ADMM_GCOL_MM=0 keeps the LDS column pass,
+// ADMM_GCOL_MM_NL the columns per block (8 or 16)
+MMPlan mm_plan(int H, int W) {
+    MMPlan m{};
+    if (!env_int("ADMM_GCOL_MM", 1) || H < 17) return m;
+    int r = H, big = 1;  // largest prime factor of H
+    for (int f = 2; f * f <= r; ++f)
+        while (r % f == 0) {
+            big = std::max(big, f);
+            r /= f;
+        }
+    big = std::max(big, r);
+    if (big < 17 || big > 127) return m;
+    for (int S = 1; S <= 8; ++S) {
+        if (S == 7 || H % S) continue;  // instances: S = 1..6, 8
+        const int R = H / S;
+        if (R > 127 || !(R & 1) || R % big) continue;
+        m.R = R;
+        m.S = S;
+        break;
+    }
+    if (!m.R) return m;
+    m.h = (m.R - 1) / 2;
+    m.KS = (m.h + 1 + 3) / 4;
+    m.MT = (m.h + 1 + 15) / 16;
+    const int G = m.MT == 3 ? 1 : 4 / m.MT;
+    int NL = env_int("ADMM_GCOL_MM_NL", 16) >= 16 ? 16 : 8;
+    while (NL < 16 && (NL * m.S) % 8) NL *= 2;
+    // n-tiles of 16 real columns: NL S / 8 of them, at most 8 per wave (the accumulator arrays)
+    while (NL > 8 && ((NL * m.S / 8) + G - 1) / G > 8) NL /= 2;
+    if ((NL * m.S) % 8 || ((NL * m.S / 8) + G - 1) / G > 8) return m;
+    m.NL = NL;
+    m.RP = 4 * NL * m.S;
+    while (m.RP % 64 != 32) m.RP += 16;
+    m.lds = (size_t)4 * m.KS * m.RP * sizeof(float) + (size_t)H * sizeof(cf);  // image + twiddles
+    m.ok = m.lds <= kMaxLds;
+    (void)W;
+    return m;
+}
+
 // the launchers below are templated on the real type T of the solve: float, or double for fp64
 // inputs (ADMM_TV_FLAG_F64: the generic kernels' double instantiation, plans without Bluestein
 // stages, 256-thread blocks)
@@ -1026,9 +1081,31 @@ int gcol_launch(const GColArgsT<T>& a, size_t lds, dim3 grid, hipStream_t s) {
                        dim3(kF64<T> || GLB ? GNT : gen_threads("ADMM_GCOL_NT")), lds, s, a);
     return launch_check("k_gcol");
 }
+template <int S> int gcol_mm_launch(const GColMMArgs& a, size_t lds, hipStream_t s) {
+    if (int e = set_lds(k_gcol_mm<S>, lds)) return e;
+    hipLaunchKernelGGL(k_gcol_mm<S>, dim3((unsigned)(a.P * a.colblocks)), dim3(256), lds, s, a);
+    return launch_check("k_gcol_mm");
+}
 template <class T>
 int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx_t<T>* tw, int H, int W, long long P,
          int mode, hipStream_t s, cx_t<T>* gscr = nullptr) {
+    if constexpr (!kF64<T>) {
+        const MMPlan m = mm_plan(H, W);
+        if (mode == 0 && m.ok) {  // the factor's [H][Wh] copy follows fcT (setup, k_fc_transpose)
+            const int Wh = W / 2 + 1;
+            GColMMArgs a{spec, dump, fcT + (size_t)Wh * H, tw, H, m.R, m.h, m.KS, m.MT, m.NL, __builtin_ctz(m.NL), m.RP,
+                         Wh, (Wh + m.NL - 1) / m.NL, P};
+            switch (m.S) {
+                case 1: return gcol_mm_launch<1>(a, m.lds, s);
+                case 2: return gcol_mm_launch<2>(a, m.lds, s);
+                case 3: return gcol_mm_launch<3>(a, m.lds, s);
+                case 4: return gcol_mm_launch<4>(a, m.lds, s);
+                case 5: return gcol_mm_launch<5>(a, m.lds, s);
+                case 6: return gcol_mm_launch<6>(a, m.lds, s);
+                default: return gcol_mm_launch<8>(a, m.lds, s);
+            }
+        }
+    }
     const GPlan pl = make_plan(H, kF64<T>);
     GLB_CHECK(pl, gscr)
     const int Wh = W / 2 + 1, cols = gcol_cols(H, pl, kCsz<T>);
