@@ -1,6 +1,7 @@
-"""The matrix-core column pass (csrc/gcol_mm.hpp, k_gcol_mm): column lengths H = S * R with an odd
-R in [17, 127] that carries H's largest prime factor run their R-point transforms as cosine / sine
-matrix products on v_mfma_f32_16x16x4_f32 (BSD: 321 = 3 * 107).
+"""The matrix-core transforms (csrc/gcol_mm.hpp): column lengths H = S * R with an odd R in
+[17, 127] that carries H's largest prime factor run their R-point transforms as cosine / sine matrix
+products on v_mfma_f32_16x16x4_f32 (k_gcol_mm; BSD: 321 = 3 * 107), and so do the row inverses of
+row lengths W = S * R (k_grow_inv_mm; BSD: 481 = 13 * 37).
 
 Parity as for the rest of the generic path (test_gpu_generic.py): rel-L2 <= 1e-5 against the fp64
 oracle, which is pinned to the reference (tests/test_oracle_golden.py); the reference's own x-update is
@@ -51,6 +52,36 @@ def test_mm_column_pass_vs_oracle(cuda_dev, shape, psf, iso, monkeypatch):
     assert e <= TOL_REF64
     assert e <= 2 * e_lds + 1e-6
     assert not torch.equal(got, lds)  # the two passes round differently: the matrix-core one ran
+
+
+# row lengths W = S * R for the matrix-core row inverse (k_grow_inv_mm); odd row counts leave the last
+# line of a batch with one real row
+ROW_SHAPES = [
+    ((1, 2, 9, 107), ("gauss:1.0", 5), False),    # S 1, R 107 (odd row count: 18 rows)
+    ((2, 1, 7, 214), ("gauss:1.5", 7), True),     # S 2
+    ((1, 3, 20, 321), ("gauss:1.5", 9), False),   # S 3
+    ((1, 1, 15, 148), ("motion", 7), False),      # S 4, R 37
+    ((1, 1, 12, 115), ("gauss:1.0", 5), True),    # S 5, R 23
+    ((1, 1, 11, 136), ("gauss:1.5", 9), False),   # S 8, R 17
+    ((1, 3, 33, 481), ("gauss:1.5", 9), False),   # S 13, R 37: the BSD rows
+    ((1, 1, 5, 221), ("motion", 5), True),        # S 13, R 17
+    ((1, 1, 13, 127), ("gauss:2", 9), False),     # S 1, R 127: 4 row tiles
+    ((3, 1, 1, 93), None, False),                 # one-row planes, R 93 = 3 * 31
+]
+
+
+@pytest.mark.parametrize("shape,psf,iso", ROW_SHAPES)
+def test_mm_row_inverse_vs_oracle(cuda_dev, shape, psf, iso, monkeypatch):
+    x, k = _x(shape, psf, sum(shape) + 1)
+    ref = oracle(x, k, 0.01, 0.02, iso, 15)
+    got = solve(x, k, 0.01, 0.02, iso, 15, cuda_dev)
+    monkeypatch.setenv("ADMM_GROW_MM", "0")
+    lds = solve(x, k, 0.01, 0.02, iso, 15, cuda_dev)
+    e, e_lds = rel(got, ref), rel(lds, ref)
+    print(shape, psf, "iso" if iso else "aniso", f"matrix-core rows {e:.3e}  LDS rows {e_lds:.3e}")
+    assert e <= TOL_REF64
+    assert e <= 2 * e_lds + 1e-6
+    assert not torch.equal(got, lds)
 
 
 def test_mm_bsd_batch_sampled_planes(cuda_dev):

@@ -125,6 +125,7 @@ struct MMPlan {
     size_t lds;
 };
 MMPlan mm_plan(int H, int W);
+MMPlan mm_plan_row(int W);  // the row inverse (k_grow_inv_mm): W = S R, S in {1..5, 8, 13}
 
 // modules solved together (admm_tv_desc.groups)
 int ngroups_of(const admm_tv_desc& d) { return d.groups > 1 ? d.groups : 1; }
@@ -949,16 +950,54 @@ MMPlan mm_plan(int H, int W) {
     m.MT = (m.h + 1 + 15) / 16;
     const int G = m.MT == 3 ? 1 : 4 / m.MT;
     int NL = env_int("ADMM_GCOL_MM_NL", 16) >= 16 ? 16 : 8;
-    while (NL < 16 && (NL * m.S) % 8) NL *= 2;
-    // n-tiles of 16 real columns: NL S / 8 of them, at most 8 per wave (the accumulator arrays)
-    while (NL > 8 && ((NL * m.S / 8) + G - 1) / G > 8) NL /= 2;
-    if ((NL * m.S) % 8 || ((NL * m.S / 8) + G - 1) / G > 8) return m;
+    // n-tiles of 16 real columns: ceil(NL S / 8) of them (the last one padded), at most 8 per wave (the
+    // accumulator arrays)
+    while (NL > 1 && ((NL * m.S + 7) / 8 + G - 1) / G > 8) NL /= 2;
+    if (((NL * m.S + 7) / 8 + G - 1) / G > 8) return m;
     m.NL = NL;
-    m.RP = 4 * NL * m.S;
+    m.RP = std::max(4 * NL * m.S, 32 * ((NL * m.S + 7) / 8));
     while (m.RP % 64 != 32) m.RP += 16;
     m.lds = (size_t)4 * m.KS * m.RP * sizeof(float) + (size_t)H * sizeof(cf);  // image + twiddles
     m.ok = m.lds <= kMaxLds;
     (void)W;
+    return m;
+}
+
+// row inverse on the matrix cores: lines (row pairs) per block NL, one (line, k1) item per thread,
+// at most 8 n-tiles per wave.  A/B knob: ADMM_GROW_MM=0 keeps the LDS row inverse.
+MMPlan mm_plan_row(int W) {
+    MMPlan m{};
+    if (!env_int("ADMM_GROW_MM", 1) || W < 17) return m;
+    int r = W, big = 1;
+    for (int f = 2; f * f <= r; ++f)
+        while (r % f == 0) {
+            big = std::max(big, f);
+            r /= f;
+        }
+    big = std::max(big, r);
+    if (big < 17 || big > 127) return m;
+    for (int S : {1, 2, 3, 4, 5, 8, 13}) {
+        if (W % S) continue;
+        const int R = W / S;
+        if (R > 127 || !(R & 1) || R % big) continue;
+        m.R = R;
+        m.S = S;
+        break;
+    }
+    if (!m.R) return m;
+    m.h = (m.R - 1) / 2;
+    m.KS = (m.h + 1 + 3) / 4;
+    m.MT = (m.h + 1 + 15) / 16;
+    const int G = m.MT == 3 ? 1 : 4 / m.MT;
+    int NL = 16;
+    while (NL > 1 && (NL * (m.h + 1) > 256 || ((NL * m.S + 7) / 8 + G - 1) / G > 8)) NL /= 2;
+    if (NL * (m.h + 1) > 256 || ((NL * m.S + 7) / 8 + G - 1) / G > 8) return m;  // one (line, k1) item per thread
+    m.NL = NL;
+    m.RP = std::max(4 * NL * m.S, 32 * ((NL * m.S + 7) / 8));
+    while (m.RP % 64 != 32) m.RP += 16;
+    const size_t stage = (size_t)2 * NL * (W / 2 + 1) * 2;  // floats
+    m.lds = std::max(stage, (size_t)4 * m.KS * m.RP) * sizeof(float) + (size_t)W * sizeof(cf);
+    m.ok = m.lds <= kMaxLds;
     return m;
 }
 
@@ -1043,9 +1082,30 @@ int grow_fwd_step(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int 
     return first ? grow_fwd_step_t<false, true>(g, spec, tw, W, rows, s, gscr)
                  : grow_fwd_step_t<false, false>(g, spec, tw, W, rows, s, gscr);
 }
+template <int S> int grow_inv_mm_launch(const GRowInvMMArgs& a, size_t lds, hipStream_t s) {
+    if (int e = set_lds(k_grow_inv_mm<S>, lds)) return e;
+    hipLaunchKernelGGL(k_grow_inv_mm<S>, dim3((unsigned)((a.rows + 2 * a.NL - 1) / (2 * a.NL))), dim3(256), lds, s, a);
+    return launch_check("k_grow_inv_mm");
+}
 template <class T>
 int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long rows, hipStream_t s,
              cx_t<T>* gscr = nullptr) {
+    if constexpr (!kF64<T>) {
+        const MMPlan m = mm_plan_row(W);
+        if (m.ok && rows > 0) {
+            const int Wh = W / 2 + 1;
+            GRowInvMMArgs a{spec, img, tw, rows, W, m.R, m.h, m.KS, m.MT, m.NL, m.RP, Wh, 2 * m.NL * Wh * 2};
+            switch (m.S) {
+                case 1: return grow_inv_mm_launch<1>(a, m.lds, s);
+                case 2: return grow_inv_mm_launch<2>(a, m.lds, s);
+                case 3: return grow_inv_mm_launch<3>(a, m.lds, s);
+                case 4: return grow_inv_mm_launch<4>(a, m.lds, s);
+                case 5: return grow_inv_mm_launch<5>(a, m.lds, s);
+                case 8: return grow_inv_mm_launch<8>(a, m.lds, s);
+                default: return grow_inv_mm_launch<13>(a, m.lds, s);
+            }
+        }
+    }
     const GPlan pl = make_plan(W, kF64<T>);
     GLB_CHECK(pl, gscr)
     GRowArgsT<T> a{nullptr, const_cast<cx_t<T>*>(spec), img, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr};
@@ -1094,7 +1154,7 @@ int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx
         if (mode == 0 && m.ok) {  // the factor's [H][Wh] copy follows fcT (setup, k_fc_transpose)
             const int Wh = W / 2 + 1;
             GColMMArgs a{spec, dump, fcT + (size_t)Wh * H, tw, H, m.R, m.h, m.KS, m.MT, m.NL, __builtin_ctz(m.NL), m.RP,
-                         Wh, (Wh + m.NL - 1) / m.NL, P};
+                         Wh, (Wh + m.NL - 1) / m.NL, P, env_int("ADMM_MM_DBG", 0)};
             switch (m.S) {
                 case 1: return gcol_mm_launch<1>(a, m.lds, s);
                 case 2: return gcol_mm_launch<2>(a, m.lds, s);

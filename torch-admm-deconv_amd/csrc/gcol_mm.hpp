@@ -39,6 +39,7 @@ struct GColMMArgs {
     const cf* tw;      // [H] exp(-2 pi i m / H)
     int H, R, h, KS, MT, NL, lgNL, RP, Wh, colblocks;
     long long P;
+    int dbg;  // timing experiments only (ADMM_MM_DBG): phases to skip, results invalid when set
 };
 
 typedef float mm_f32x4 __attribute__((ext_vector_type(4)));
@@ -157,7 +158,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
     cf* twl = reinterpret_cast<cf*>(F + 4 * KS * RP);       // the H twiddles, after the image
 
     // wave -> (row tile mt, n-tiles tile0, tile0 + tstep, ...): MT row tiles of 16, G waves per tile
-    const int NT = NL * S / 8;
+    const int NT = (NL * S + 7) / 8;  // n-tiles of 16 real columns (the last one padded)
     const int G = MT == 3 ? 1 : 4 / MT;
     const bool gw = wv < MT * G;
     const int mt = wv % MT, tile0 = wv / MT, tstep = G;
@@ -174,7 +175,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
             const int L = it & (NL - 1), rest = it >> a.lgNL;
             const int n2 = rest % S, q = rest / S;
             x0[u] = x1[u] = mkc(0.f, 0.f);
-            if (it < nload && c0 + L < Wh) {
+            if (!(a.dbg & 8) && it < nload && c0 + L < Wh) {
                 x0[u] = Sp[(size_t)(n2 + S * q) * Wh + L];
                 if (q) x1[u] = Sp[(size_t)(n2 + S * (R - q)) * Wh + L];
             }
@@ -194,24 +195,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
     // rows h+1 .. 4 KS - 1 are the k-steps' padding: zero (their matrix entries are zero too)
     for (int idx = tid; idx < (4 * KS - h - 1) * RP; idx += 256) F[(h + 1) * RP + idx] = 0.f;
 
+    __syncthreads();
+
     // this lane's fragments of the cosine / sine matrices: A[i = lane & 15][q = lane >> 4] of each
-    // 16 x 4 k-step; cos / sin(2 pi m / R) = Re / -Im tw[m S]
+    // 16 x 4 k-step; cos / sin(2 pi m / R) = Re / -Im tw[m S], m = i q mod R stepped by 4 i mod R
     float a1[16], a2[16];
     {
         const int i = 16 * mt + jl;
+        const int step = (4 * i) % R;
+        int m = (i * g) % R;
         static_for<0, 16>([&](auto kc) {
             constexpr int ks = decltype(kc)::value;
             const int q = 4 * ks + g;
             const bool ok = gw && ks < KS && i <= h && q <= h;
-            const cf w = ok ? a.tw[((i * q) % R) * S] : mkc(0.f, 0.f);
+            const cf w = ok ? twl[m * S] : mkc(0.f, 0.f);
             a1[ks] = w.x;
             a2[ks] = -w.y;
+            m += step;
+            m -= (m >= R) ? R : 0;
         });
     }
-    __syncthreads();
-
     mm_f32x4 acc1[8], acc2[8];  // (the entries a wave's tile count uses)
-    mm_ntw(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
+    if (!(a.dbg & 1)) mm_ntw(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
     __syncthreads();  // every operand read before the outputs overwrite them
     mm_ntw(ntw, [&](auto nc) { mm_store<-1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
 
@@ -238,7 +243,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
     static_for<0, 4>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         const int it = tid + 256 * u;
-        if (it < nmid) {
+        if (!(a.dbg & 4) && it < nmid) {
             if constexpr (u >= MI) load_f(uc);
             const int L = it & (NL - 1), k1 = it >> a.lgNL;
             const int kx = c0 + L;
@@ -263,7 +268,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
     });
     __syncthreads();
 
-    mm_ntw(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
+    if (!(a.dbg & 2)) mm_ntw(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
     __syncthreads();
     mm_ntw(ntw, [&](auto nc) { mm_store<+1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
     __syncthreads();
@@ -273,10 +278,137 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
     for (int it = tid; it < nout; it += 256) {
         const int L = it & (NL - 1), rest = it >> a.lgNL;
         const int n2 = rest % S, n1 = rest / S;
-        if (c0 + L >= Wh) continue;
+        if (c0 + L >= Wh || (a.dbg & 16)) continue;
         const float4 v = *reinterpret_cast<const float4*>(&F[n1 * RP + 4 * (n2 * NL + L)]);
         Sp[(size_t)(n2 + S * n1) * Wh + L] = mkc(v.x, v.z);
         if (n1) Sp[(size_t)(n2 + S * (R - n1)) * Wh + L] = mkc(v.y, v.w);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row inverse on the matrix cores (k_grow_inv_mm): half spectra -> real rows for row lengths
+// W = S R (BSD: 481 = 13 * 37), the k_grow_inv contract (generic_kernels.hpp): two real rows a, b of
+// a line as one complex sequence Z = Xa + i Xb with Hermitian completion (the imaginary parts of the
+// self-conjugate bins dropped, as irfft does), its inverse DFT z = xa + i xb.
+// Input index k = k1 + R k2, output n = n2 + S n1:
+//   1. per (line, k1 <= h): Z[k1 + R k2] and Z[R - k1 + R k2] (k2 < S) from the staged half
+//      spectra, inverse S-point DFT over k2, conjugate twiddle W_W^{-n2 k}, sums / differences
+//   2. inverse R-point transforms as the cosine / sine matrix products (as k_gcol_mm)
+//   3. rows a and b of every line written along n (coalesced)
+// LDS: the block's 2 NL spectrum rows, then (aliased) the matrix image, columns seq = l S + n2.
+// ---------------------------------------------------------------------------------------------
+struct GRowInvMMArgs {
+    const cf* spec;  // [rows][Wh]
+    float* img;      // [rows][W]
+    const cf* tw;    // [W] exp(-2 pi i m / W)
+    long long rows;
+    int W, R, h, KS, MT, NL, RP, Wh;
+    int stage;       // floats of the staged spectrum rows (the image region starts at 0 too)
+};
+
+template <int S>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_grow_inv_mm(GRowInvMMArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float F[];
+    const int W = a.W, R = a.R, h = a.h, NL = a.NL, RP = a.RP, KS = a.KS, MT = a.MT, Wh = a.Wh;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int jl = lane & 15, g = lane >> 4;
+    const long long r0 = (long long)blockIdx.x * 2 * NL;
+    const int nrows = (int)min((long long)2 * NL, a.rows - r0);
+    const int regn = max(a.stage, 4 * KS * RP);
+    cf* Xs = reinterpret_cast<cf*>(F);        // staged spectrum rows [2 NL][Wh]
+    cf* twl = reinterpret_cast<cf*>(F + regn);
+
+    const int NT = (NL * S + 7) / 8;  // n-tiles of 16 real columns (the last one padded)
+    const int G = MT == 3 ? 1 : 4 / MT;
+    const bool gw = wv < MT * G;
+    const int mt = wv % MT, tile0 = wv / MT, tstep = G;
+    const int ntw = gw ? (NT - tile0 + G - 1) / G : 0;
+
+    {   // stage: the block's rows are contiguous in the spectrum
+        const cf* src = a.spec + r0 * Wh;
+        const int n = nrows * Wh;
+        for (int i = tid; i < n; i += 256) Xs[i] = src[i];
+        for (int i = nrows * Wh + tid; i < 2 * NL * Wh; i += 256) Xs[i] = mkc(0.f, 0.f);
+        for (int i = tid; i < W; i += 256) twl[i] = a.tw[i];
+    }
+    __syncthreads();
+
+    // Z[k] of line l from its two staged rows (Hermitian completion)
+    auto zval = [&](int l, int k) -> cf {
+        const bool lo = k < Wh;
+        const int kk = lo ? k : W - k;
+        cf xa = Xs[(2 * l) * Wh + kk], xb = Xs[(2 * l + 1) * Wh + kk];
+        if (kk == 0 || 2 * kk == W) xa.y = xb.y = 0.f;
+        if (!lo) xa.y = -xa.y, xb.y = -xb.y;
+        return mkc(xa.x - xb.y, xa.y + xb.x);
+    };
+    // phase 1: one item (l, k1) per thread (NL (h + 1) <= 256), kept in registers until the image may
+    // overwrite the staged rows
+    const int nmid = NL * (h + 1);
+    float4 sd[S];
+    const int l1 = tid % NL, k1 = tid / NL;
+    if (tid < nmid) {
+        cf v[S], vr[S];
+#pragma unroll
+        for (int k2 = 0; k2 < S; ++k2) {
+            v[k2] = zval(l1, k1 + R * k2);
+            vr[k2] = k1 ? zval(l1, R - k1 + R * k2) : mkc(0.f, 0.f);
+        }
+        small_dft<+1, S>(v, twl, W);
+        small_dft<+1, S>(vr, twl, W);
+#pragma unroll
+        for (int n2 = 1; n2 < S; ++n2) {
+            v[n2] = cmulc(v[n2], twl[n2 * k1]);
+            if (k1) vr[n2] = cmulc(vr[n2], twl[n2 * (R - k1)]);
+        }
+#pragma unroll
+        for (int n2 = 0; n2 < S; ++n2) {
+            const cf x = v[n2], y = vr[n2];
+            sd[n2] = k1 ? make_float4(x.x + y.x, x.x - y.x, x.y + y.y, x.y - y.y) : make_float4(x.x, 0.f, x.y, 0.f);
+        }
+    }
+    __syncthreads();
+    if (tid < nmid) {
+#pragma unroll
+        for (int n2 = 0; n2 < S; ++n2) *reinterpret_cast<float4*>(&F[k1 * RP + 4 * (l1 * S + n2)]) = sd[n2];
+    }
+    for (int idx = tid; idx < (4 * KS - h - 1) * RP; idx += 256) F[(h + 1) * RP + idx] = 0.f;
+    __syncthreads();
+
+    float a1[16], a2[16];
+    {
+        const int i = 16 * mt + jl;
+        const int step = (4 * i) % R;
+        int m = (i * g) % R;
+        static_for<0, 16>([&](auto kc) {
+            constexpr int ks = decltype(kc)::value;
+            const int q = 4 * ks + g;
+            const bool ok = gw && ks < KS && i <= h && q <= h;
+            const cf w = ok ? twl[m * S] : mkc(0.f, 0.f);
+            a1[ks] = w.x;
+            a2[ks] = -w.y;
+            m += step;
+            m -= (m >= R) ? R : 0;
+        });
+    }
+    mm_f32x4 acc1[8], acc2[8];
+    mm_ntw(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
+    __syncthreads();
+    mm_ntw(ntw, [&](auto nc) { mm_store<+1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
+    __syncthreads();
+
+    // phase 3: z[n] of line l at n = n2 + S n1: (n1 <= h) slot 0 of row n1, else slot 1 of row R - n1
+    for (int l = 0; l < NL && 2 * l < nrows; ++l) {
+        float* dst = a.img + (r0 + 2 * l) * W;
+        const bool two = 2 * l + 1 < nrows;
+        for (int n = tid; n < W; n += 256) {
+            const int n1 = n / S, n2 = n - n1 * S;
+            const bool lo = n1 <= h;
+            const float* e = &F[(lo ? n1 : R - n1) * RP + 4 * (l * S + n2) + (lo ? 0 : 1)];
+            dst[n] = e[0];
+            if (two) dst[W + n] = e[2];
+        }
     }
 }
 
