@@ -1142,8 +1142,18 @@ int gcol_launch(const GColArgsT<T>& a, size_t lds, dim3 grid, hipStream_t s) {
     return launch_check("k_gcol");
 }
 template <int S> int gcol_mm_launch(const GColMMArgs& a, size_t lds, hipStream_t s) {
+    const dim3 grid((unsigned)(a.P * a.colblocks));
+    // 512-thread blocks for S <= 4 (NL = 16: at most 8 n-tiles, 2+ waves per row tile -> at most 4 per
+    // wave; BSD 4,191-4,230 -> 4,343-4,354 it/s, profiles/r03_gcol_mm_nt.txt); A/B knob ADMM_GCOL_MM_NT
+    if constexpr (S <= 4) {
+        if (a.NL == 16 && env_int("ADMM_GCOL_MM_NT", 512) == 512) {
+            if (int e = set_lds(k_gcol_mm<S, 512>, lds)) return e;
+            hipLaunchKernelGGL((k_gcol_mm<S, 512>), grid, dim3(512), lds, s, a);
+            return launch_check("k_gcol_mm");
+        }
+    }
     if (int e = set_lds(k_gcol_mm<S>, lds)) return e;
-    hipLaunchKernelGGL(k_gcol_mm<S>, dim3((unsigned)(a.P * a.colblocks)), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(k_gcol_mm<S>, grid, dim3(256), lds, s, a);
     return launch_check("k_gcol_mm");
 }
 template <class T>

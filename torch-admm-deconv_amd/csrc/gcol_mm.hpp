@@ -104,17 +104,18 @@ __device__ __forceinline__ void mm_store(float* __restrict__ F, const mm_f32x4 (
     });
 }
 
-// runs f(integral_constant NTW) for the wave's tile count (wave-uniform, 0: no call)
-template <class Fn> __device__ __forceinline__ void mm_ntw(int ntw, Fn&& f) {
+// runs f(integral_constant NTW) for the wave's tile count (wave-uniform, 0: no call); instances up to
+// MAXT (the accumulator registers of the largest instance are reserved for all)
+template <int MAXT = 8, class Fn> __device__ __forceinline__ void mm_ntw(int ntw, Fn&& f) {
     switch (ntw) {
         case 1: f(std::integral_constant<int, 1>{}); break;
         case 2: f(std::integral_constant<int, 2>{}); break;
-        case 3: f(std::integral_constant<int, 3>{}); break;
-        case 4: f(std::integral_constant<int, 4>{}); break;
-        case 5: f(std::integral_constant<int, 5>{}); break;
-        case 6: f(std::integral_constant<int, 6>{}); break;
-        case 7: f(std::integral_constant<int, 7>{}); break;
-        case 8: f(std::integral_constant<int, 8>{}); break;
+        case 3: if constexpr (MAXT >= 3) f(std::integral_constant<int, 3>{}); break;
+        case 4: if constexpr (MAXT >= 4) f(std::integral_constant<int, 4>{}); break;
+        case 5: if constexpr (MAXT >= 5) f(std::integral_constant<int, 5>{}); break;
+        case 6: if constexpr (MAXT >= 6) f(std::integral_constant<int, 6>{}); break;
+        case 7: if constexpr (MAXT >= 7) f(std::integral_constant<int, 7>{}); break;
+        case 8: if constexpr (MAXT >= 8) f(std::integral_constant<int, 8>{}); break;
         default: break;
     }
 }
@@ -143,8 +144,11 @@ __device__ __forceinline__ void mm_column_mid(cf (&v)[S], const float (&f)[S], i
 // items per thread of the load / store loops whose global accesses are issued together
 constexpr int kMMU = 4;
 
-template <int S>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3 ? 3 : 2))) k_gcol_mm(GColMMArgs a) {
+// NTH threads per block (256 or 512, ADMM_GCOL_MM_NT): with 512 the waves of a row tile split its n-tiles
+// (fewer accumulators per wave) and more waves per CU are resident
+template <int S, int NTH = 256>
+__global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 512 ? 4 : (S <= 3 ? 3 : 2))))
+k_gcol_mm(GColMMArgs a) {
     extern __shared__ __attribute__((aligned(16))) float F[];
     const int H = a.H, R = a.R, h = a.h, NL = a.NL, RP = a.RP, KS = a.KS, MT = a.MT, Wh = a.Wh;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -159,7 +163,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
 
     // wave -> (row tile mt, n-tiles tile0, tile0 + tstep, ...): MT row tiles of 16, G waves per tile
     const int NT = (NL * S + 7) / 8;  // n-tiles of 16 real columns (the last one padded)
-    const int G = MT == 3 ? 1 : 4 / MT;
+    const int G = (NTH / 64) / MT;  // waves per row tile
     const bool gw = wv < MT * G;
     const int mt = wv % MT, tile0 = wv / MT, tstep = G;
     const int ntw = gw ? (NT - tile0 + G - 1) / G : 0;
@@ -167,11 +171,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
     // load: s_q, d_q of every sequence (L, n2), straight from the spectrum (rows of NL columns); a
     // thread's kMMU items issue their loads together
     const int nload = NL * S * (h + 1);
-    for (int base = tid; base < nload; base += 256 * kMMU) {
+    for (int base = tid; base < nload; base += NTH * kMMU) {
         cf x0[kMMU], x1[kMMU];
         static_for<0, kMMU>([&](auto uc) {
             constexpr int u = decltype(uc)::value;
-            const int it = base + 256 * u;
+            const int it = base + NTH * u;
             const int L = it & (NL - 1), rest = it >> a.lgNL;
             const int n2 = rest % S, q = rest / S;
             x0[u] = x1[u] = mkc(0.f, 0.f);
@@ -182,7 +186,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
         });
         static_for<0, kMMU>([&](auto uc) {
             constexpr int u = decltype(uc)::value;
-            const int it = base + 256 * u;
+            const int it = base + NTH * u;
             const int L = it & (NL - 1), rest = it >> a.lgNL;
             const int n2 = rest % S, q = rest / S;
             if (it < nload)
@@ -191,9 +195,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
                       : make_float4(x0[u].x, 0.f, x0[u].y, 0.f);
         });
     }
-    for (int i = tid; i < H; i += 256) twl[i] = a.tw[i];
+    for (int i = tid; i < H; i += NTH) twl[i] = a.tw[i];
     // rows h+1 .. 4 KS - 1 are the k-steps' padding: zero (their matrix entries are zero too)
-    for (int idx = tid; idx < (4 * KS - h - 1) * RP; idx += 256) F[(h + 1) * RP + idx] = 0.f;
+    for (int idx = tid; idx < (4 * KS - h - 1) * RP; idx += NTH) F[(h + 1) * RP + idx] = 0.f;
 
     __syncthreads();
 
@@ -216,19 +220,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
         });
     }
     mm_f32x4 acc1[8], acc2[8];  // (the entries a wave's tile count uses)
-    if (!(a.dbg & 1)) mm_ntw(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
+    if (!(a.dbg & 1)) mm_ntw<NTH == 512 ? 4 : (2 * S < 8 ? 2 * S : 8)>(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
     __syncthreads();  // every operand read before the outputs overwrite them
-    mm_ntw(ntw, [&](auto nc) { mm_store<-1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
+    mm_ntw<NTH == 512 ? 4 : (2 * S < 8 ? 2 * S : 8)>(ntw, [&](auto nc) { mm_store<-1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
 
     // per (column L, k1 <= h): outputs k1 and R - k1 of all S sequences -> factor -> inverse
     // inputs, stored as the sums / differences the inverse R-point transforms take.  A thread has at
-    // most 4 such items (NL (h + 1) <= 1,024); their factors are loaded before the barrier.
+    // most MAXI such items (NL (h + 1) <= 1,024); their factors are loaded before the barrier.
     const int nmid = NL * (h + 1);
-    constexpr int MI = S <= 4 ? 4 : 2;  // items whose factors are prefetched (registers)
-    float fk[4][S], fr[4][S];
+    constexpr int MAXI = 1024 / NTH;                    // items per thread at most
+    constexpr int MI = S <= 4 ? MAXI : (MAXI < 2 ? MAXI : 2);  // items whose factors are prefetched
+    float fk[MAXI][S], fr[MAXI][S];
     auto load_f = [&](auto uc) {
         constexpr int u = decltype(uc)::value;
-        const int it = tid + 256 * u;
+        const int it = tid + NTH * u;
         const int L = it & (NL - 1), k1 = it >> a.lgNL;
         const int kx = c0 + L;
         const bool ok = it < nmid && kx < Wh;
@@ -240,9 +245,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
     };
     static_for<0, MI>(load_f);
     __syncthreads();
-    static_for<0, 4>([&](auto uc) {
+    static_for<0, MAXI>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
-        const int it = tid + 256 * u;
+        const int it = tid + NTH * u;
         if (!(a.dbg & 4) && it < nmid) {
             if constexpr (u >= MI) load_f(uc);
             const int L = it & (NL - 1), k1 = it >> a.lgNL;
@@ -268,14 +273,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 3
     });
     __syncthreads();
 
-    if (!(a.dbg & 2)) mm_ntw(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
+    if (!(a.dbg & 2)) mm_ntw<NTH == 512 ? 4 : (2 * S < 8 ? 2 * S : 8)>(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
     __syncthreads();
-    mm_ntw(ntw, [&](auto nc) { mm_store<+1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
+    mm_ntw<NTH == 512 ? 4 : (2 * S < 8 ? 2 * S : 8)>(ntw, [&](auto nc) { mm_store<+1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
     __syncthreads();
 
     // store: x[n2 + S n1] and x[n2 + S (R - n1)] of every sequence
     const int nout = NL * S * (h + 1);
-    for (int it = tid; it < nout; it += 256) {
+    for (int it = tid; it < nout; it += NTH) {
         const int L = it & (NL - 1), rest = it >> a.lgNL;
         const int n2 = rest % S, n1 = rest / S;
         if (c0 + L >= Wh || (a.dbg & 16)) continue;
