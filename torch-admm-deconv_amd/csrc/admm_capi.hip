@@ -123,6 +123,7 @@ struct MMPlan {
     bool ok;
     int R, S, h, KS, MT, NL, RP;
     size_t lds;
+    int nth;  // threads per block (the row inverse; the column pass picks its own)
 };
 MMPlan mm_plan(int H, int W);
 MMPlan mm_plan_row(int W);  // the row inverse (k_grow_inv_mm): W = S R, S in {1..5, 8, 13}
@@ -989,9 +990,13 @@ MMPlan mm_plan_row(int W) {
     m.KS = (m.h + 1 + 3) / 4;
     m.MT = (m.h + 1 + 15) / 16;
     const int G = m.MT == 3 ? 1 : 4 / m.MT;
+    // 256-thread blocks; A/B knob ADMM_GROW_MM_NT=512: 2 G waves per row tile, at most 4 n-tiles per wave
+    // (BSD two streams 4,281-4,310 -> 4,130 it/s, profiles/r03_grow_inv_mm_nt.txt)
+    m.nth = env_int("ADMM_GROW_MM_NT", 256) == 512 ? 512 : 256;
+    const int Gt = m.nth == 512 ? 2 * G : G, maxt = m.nth == 512 ? 4 : 8;
     int NL = 16;
-    while (NL > 1 && (NL * (m.h + 1) > 256 || ((NL * m.S + 7) / 8 + G - 1) / G > 8)) NL /= 2;
-    if (NL * (m.h + 1) > 256 || ((NL * m.S + 7) / 8 + G - 1) / G > 8) return m;  // one (line, k1) item per thread
+    while (NL > 1 && (NL * (m.h + 1) > m.nth || ((NL * m.S + 7) / 8 + Gt - 1) / Gt > maxt)) NL /= 2;
+    if (NL * (m.h + 1) > m.nth || ((NL * m.S + 7) / 8 + Gt - 1) / Gt > maxt) return m;  // one (line, k1) item per thread
     m.NL = NL;
     m.RP = std::max(4 * NL * m.S, 32 * ((NL * m.S + 7) / 8));
     while (m.RP % 64 != 32) m.RP += 16;
@@ -1082,9 +1087,15 @@ int grow_fwd_step(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int 
     return first ? grow_fwd_step_t<false, true>(g, spec, tw, W, rows, s, gscr)
                  : grow_fwd_step_t<false, false>(g, spec, tw, W, rows, s, gscr);
 }
-template <int S> int grow_inv_mm_launch(const GRowInvMMArgs& a, size_t lds, hipStream_t s) {
+template <int S> int grow_inv_mm_launch(const GRowInvMMArgs& a, size_t lds, int nth, hipStream_t s) {
+    const dim3 grid((unsigned)((a.rows + 2 * a.NL - 1) / (2 * a.NL)));
+    if (nth == 512) {
+        if (int e = set_lds(k_grow_inv_mm<S, 512>, lds)) return e;
+        hipLaunchKernelGGL((k_grow_inv_mm<S, 512>), grid, dim3(512), lds, s, a);
+        return launch_check("k_grow_inv_mm");
+    }
     if (int e = set_lds(k_grow_inv_mm<S>, lds)) return e;
-    hipLaunchKernelGGL(k_grow_inv_mm<S>, dim3((unsigned)((a.rows + 2 * a.NL - 1) / (2 * a.NL))), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(k_grow_inv_mm<S>, grid, dim3(256), lds, s, a);
     return launch_check("k_grow_inv_mm");
 }
 template <class T>
@@ -1096,13 +1107,13 @@ int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long ro
             const int Wh = W / 2 + 1;
             GRowInvMMArgs a{spec, img, tw, rows, W, m.R, m.h, m.KS, m.MT, m.NL, m.RP, Wh, 2 * m.NL * Wh * 2};
             switch (m.S) {
-                case 1: return grow_inv_mm_launch<1>(a, m.lds, s);
-                case 2: return grow_inv_mm_launch<2>(a, m.lds, s);
-                case 3: return grow_inv_mm_launch<3>(a, m.lds, s);
-                case 4: return grow_inv_mm_launch<4>(a, m.lds, s);
-                case 5: return grow_inv_mm_launch<5>(a, m.lds, s);
-                case 8: return grow_inv_mm_launch<8>(a, m.lds, s);
-                default: return grow_inv_mm_launch<13>(a, m.lds, s);
+                case 1: return grow_inv_mm_launch<1>(a, m.lds, m.nth, s);
+                case 2: return grow_inv_mm_launch<2>(a, m.lds, m.nth, s);
+                case 3: return grow_inv_mm_launch<3>(a, m.lds, m.nth, s);
+                case 4: return grow_inv_mm_launch<4>(a, m.lds, m.nth, s);
+                case 5: return grow_inv_mm_launch<5>(a, m.lds, m.nth, s);
+                case 8: return grow_inv_mm_launch<8>(a, m.lds, m.nth, s);
+                default: return grow_inv_mm_launch<13>(a, m.lds, m.nth, s);
             }
         }
     }

@@ -311,8 +311,9 @@ struct GRowInvMMArgs {
     int stage;       // floats of the staged spectrum rows (the image region starts at 0 too)
 };
 
-template <int S>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_grow_inv_mm(GRowInvMMArgs a) {
+template <int S, int NTH = 256>
+__global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 512 ? 4 : 3)))
+k_grow_inv_mm(GRowInvMMArgs a) {
     extern __shared__ __attribute__((aligned(16))) float F[];
     const int W = a.W, R = a.R, h = a.h, NL = a.NL, RP = a.RP, KS = a.KS, MT = a.MT, Wh = a.Wh;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -325,7 +326,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
     cf* twl = reinterpret_cast<cf*>(F + regn);
 
     const int NT = (NL * S + 7) / 8;  // n-tiles of 16 real columns (the last one padded)
-    const int G = MT == 3 ? 1 : 4 / MT;
+    const int G = (NTH / 64) / MT;
     const bool gw = wv < MT * G;
     const int mt = wv % MT, tile0 = wv / MT, tstep = G;
     const int ntw = gw ? (NT - tile0 + G - 1) / G : 0;
@@ -333,9 +334,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
     {   // stage: the block's rows are contiguous in the spectrum
         const cf* src = a.spec + r0 * Wh;
         const int n = nrows * Wh;
-        for (int i = tid; i < n; i += 256) Xs[i] = src[i];
-        for (int i = nrows * Wh + tid; i < 2 * NL * Wh; i += 256) Xs[i] = mkc(0.f, 0.f);
-        for (int i = tid; i < W; i += 256) twl[i] = a.tw[i];
+        for (int i = tid; i < n; i += NTH) Xs[i] = src[i];
+        for (int i = nrows * Wh + tid; i < 2 * NL * Wh; i += NTH) Xs[i] = mkc(0.f, 0.f);
+        for (int i = tid; i < W; i += NTH) twl[i] = a.tw[i];
     }
     __syncthreads();
 
@@ -348,7 +349,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
         if (!lo) xa.y = -xa.y, xb.y = -xb.y;
         return mkc(xa.x - xb.y, xa.y + xb.x);
     };
-    // phase 1: one item (l, k1) per thread (NL (h + 1) <= 256), kept in registers until the image may
+    // phase 1: one item (l, k1) per thread (NL (h + 1) <= NTH), kept in registers until the image may
     // overwrite the staged rows
     const int nmid = NL * (h + 1);
     float4 sd[S];
@@ -378,7 +379,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
 #pragma unroll
         for (int n2 = 0; n2 < S; ++n2) *reinterpret_cast<float4*>(&F[k1 * RP + 4 * (l1 * S + n2)]) = sd[n2];
     }
-    for (int idx = tid; idx < (4 * KS - h - 1) * RP; idx += 256) F[(h + 1) * RP + idx] = 0.f;
+    for (int idx = tid; idx < (4 * KS - h - 1) * RP; idx += NTH) F[(h + 1) * RP + idx] = 0.f;
     __syncthreads();
 
     float a1[16], a2[16];
@@ -398,16 +399,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
         });
     }
     mm_f32x4 acc1[8], acc2[8];
-    mm_ntw(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
+    mm_ntw<NTH == 512 ? 4 : 8>(ntw, [&](auto nc) { mm_products<decltype(nc)::value>(F, a1, a2, acc1, acc2, KS, RP, tile0, tstep, g, jl); });
     __syncthreads();
-    mm_ntw(ntw, [&](auto nc) { mm_store<+1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
+    mm_ntw<NTH == 512 ? 4 : 8>(ntw, [&](auto nc) { mm_store<+1, decltype(nc)::value>(F, acc1, acc2, h, RP, tile0, tstep, mt, g, jl); });
     __syncthreads();
 
     // phase 3: z[n] of line l at n = n2 + S n1: (n1 <= h) slot 0 of row n1, else slot 1 of row R - n1
     for (int l = 0; l < NL && 2 * l < nrows; ++l) {
         float* dst = a.img + (r0 + 2 * l) * W;
         const bool two = 2 * l + 1 < nrows;
-        for (int n = tid; n < W; n += 256) {
+        for (int n = tid; n < W; n += NTH) {
             const int n1 = n / S, n2 = n - n1 * S;
             const bool lo = n1 <= h;
             const float* e = &F[(lo ? n1 : R - n1) * RP + 4 * (l * S + n2) + (lo ? 0 : 1)];
