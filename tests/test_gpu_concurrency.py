@@ -6,10 +6,9 @@
   library keeps no per-solve global state (ABI v4 carries the all-reduce hook in the descriptor;
   the profiler totals sit behind a lock), and the Python binding binds each call's hook to that
   call's buffers only.
-* a9: the native backward is first-order (the reference's unrolled ATen graph also supports
-  create_graph=True; this build states and enforces that it does not): differentiating a gradient
-  raises, and a second backward through the same graph raises a clear error instead of reading a
-  released history.
+* a9: a gradient taken with create_graph=True keeps the native backward's values and can be
+  differentiated again (values: tests/test_gpu_second_order.py); a second backward through the same
+  graph with retain_graph=True gives the same gradient.
 """
 import threading
 
@@ -94,16 +93,21 @@ def test_profiler_totals_under_threads(cuda_dev):
     assert all(v >= 0 for v in ms)
 
 
-def test_double_backward_is_not_supported(cuda_dev):
-    """Differentiating the gradient again raises (the backward op has no autograd formula); a second
-    backward with retain_graph=True reuses the kept history and gives the same gradient."""
+def test_create_graph_first_order_values_native(cuda_dev):
+    """A gradient taken with create_graph=True has the native backward's values bit for bit (the
+    double-backward formula only adds a graph, admmtor._unrolled), can be differentiated again,
+    and a second backward with retain_graph=True reuses the kept history: same gradient."""
     from admmtor.eops.deconv import fft_admm_tv
     x, k, _ = _case(cuda_dev, True, 6)
     xg = x.clone().requires_grad_(True)
     out = fft_admm_tv(xg, 0.01, 0.02, k, True, 10)
     (g,) = torch.autograd.grad(out.square().sum(), xg, create_graph=True)
-    with pytest.raises(RuntimeError, match="no autograd formula|once_differentiable|differentiate"):
-        g.sum().backward()
+    out0 = fft_admm_tv(xg, 0.01, 0.02, k, True, 10)
+    (g0,) = torch.autograd.grad(out0.square().sum(), xg)
+    assert torch.equal(g.detach(), g0)
+    assert g.requires_grad
+    (h,) = torch.autograd.grad(g.sum(), xg)
+    assert torch.isfinite(h).all()
     out = fft_admm_tv(xg, 0.01, 0.02, k, True, 10)
     loss = out.square().sum()
     (g1,) = torch.autograd.grad(loss, xg, retain_graph=True)

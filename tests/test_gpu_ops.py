@@ -5,9 +5,8 @@
 * torch.compile(ADMMDeconv, fullgraph=True) -- the solver is one graph node, no graph break --
   with the aot_eager backend (this build ships no Triton code; inductor would generate it for the
   surrounding elementwise ops), same bits as eager, forward and backward;
-* double backward (create_graph=True) raises PyTorch's "no autograd formula" error (not
-  supported; the reference's unrolled ATen graph would allow it); retain_graph=True gives the
-  same gradients twice.
+* double backward (create_graph=True, then a backward of the gradient) runs through the backward
+  op's own autograd formula; retain_graph=True gives the same gradients twice.
 """
 import pytest
 import torch
@@ -73,14 +72,16 @@ def test_torch_compile_fullgraph_matches_eager(cuda_dev, iso, kern):
         assert torch.equal(a, b)
 
 
-def test_double_backward_raises(cuda_dev):
+def test_double_backward_through_the_op(cuda_dev):
+    """The backward op has an autograd formula: a gradient penalty differentiates (values are checked
+    against the reference's fp64 second-order gradients in tests/test_gpu_second_order.py)."""
     from admmtor.eops.deconv import fft_admm_tv
     x, k = _inputs(cuda_dev)
     x.requires_grad_(True)
     y = fft_admm_tv(x, 0.01, 0.02, k, True, 5)
     (gx,) = torch.autograd.grad(y.square().sum(), x, create_graph=True)
-    with pytest.raises(RuntimeError):
-        gx.square().sum().backward()
+    gx.square().sum().backward()
+    assert x.grad is not None and torch.isfinite(x.grad).all()
 
 
 def test_retain_graph_second_backward_same(cuda_dev):

@@ -15,12 +15,12 @@ graph, with no graph break, and the autograd formula is registered on the op its
 
 All tensor arguments share one dtype -- fp32, or fp64 for an fp64 solve (ADMM_TV_FLAG_F64: the
 reference computes in xin.dtype, so fp64 inputs get fp64 arithmetic) -- and are contiguous, on one
-ROCm device (the public wrapper in ``admmtor.eops.deconv`` stages host / half inputs).  The backward op has no autograd
-formula of its own: differentiating the gradient again (``create_graph=True`` then a second
-``backward``) raises PyTorch's "no autograd formula" error — double backward is not supported
-(the reference's unrolled ATen graph would allow it).  The cross-rank all-reduce hook of the
+ROCm device (the public wrapper in ``admmtor.eops.deconv`` stages host / half inputs).  The backward op
+has an autograd formula of its own (``admmtor._unrolled.double_backward``), so a gradient taken with
+``create_graph=True`` can be differentiated again, as through the reference's unrolled ATen graph;
+first-order values stay the native kernels'.  The cross-rank all-reduce hook of the
 sharded iso solve (``admmtor.sharded``) is a Python callable and cannot be an op argument: that
-path keeps the ``autograd.Function`` in ``admmtor._backward``.
+path keeps the ``autograd.Function`` in ``admmtor._backward`` (first order only).
 """
 from __future__ import annotations
 
@@ -184,8 +184,9 @@ def _setup_context(ctx, inputs, output):
     x, lam, rho, kern, iso, maxit, psf_grad = inputs
     _, hist = output
     ctx.iso, ctx.maxit, ctx.psf_grad = iso, maxit, psf_grad
-    # x itself is needed only by the PSF gradient (b = H_t(x) path); otherwise a 0-size stand-in
-    ctx.save_for_backward(x if (psf_grad and kern.numel() > 0) else x.new_empty((0,)), lam, rho, kern, hist)
+    # x: read by the native backward only for the PSF gradient (b = H_t(x) path); kept in every case
+    # for a double backward (a reference to the input, no copy)
+    ctx.save_for_backward(x, lam, rho, kern, hist)
 
 
 def _backward(ctx, gout, ghist):
@@ -202,3 +203,25 @@ def _backward(ctx, gout, ghist):
 
 
 torch.library.register_autograd("admm_hip::fft_admm_tv_fwd_train", _backward, setup_context=_setup_context)
+
+
+# ---------------------------------------------------------------- double backward
+def _bwd_setup_context(ctx, inputs, output):
+    gout, x, lam, rho, kern, hist, iso, maxit, psf_grad, need_x, need_s, need_k = inputs
+    ctx.iso, ctx.maxit = iso, maxit
+    ctx.produced = (need_x, need_s, need_s, need_k)
+    ctx.save_for_backward(gout, x, lam, rho, kern)
+
+
+def _bwd_backward(ctx, ggx, ggl, ggr, ggk):
+    """Derivative of admm_tv_backward's result (admmtor._unrolled: the first-order gradient rebuilt
+    on a differentiable restatement of the same iteration, deconv.py:103-115)."""
+    from ._unrolled import double_backward
+    gout, x, lam, rho, kern = ctx.saved_tensors
+    wanted = tuple(ctx.needs_input_grad[:5])
+    grads = double_backward(gout, x, lam, rho, kern, ctx.iso, ctx.maxit, ctx.produced,
+                            (ggx, ggl, ggr, ggk), wanted)
+    return grads + (None,) * 7
+
+
+torch.library.register_autograd("admm_hip::fft_admm_tv_bwd", _bwd_backward, setup_context=_bwd_setup_context)
