@@ -499,6 +499,59 @@ __global__ void __launch_bounds__(256) k_mimic_all16(const cf* __restrict__ sp, 
     }
 }
 
+// column-strip spectrum layout [P][N/S][H][S] (S columns per strip, full height; u and b row-major):
+// pass A's row reads are N/S pieces of 8S bytes, pass B's column blocks read contiguous strips
+template <int S> __device__ __forceinline__ size_t soff(int H, int row, int col) {
+    return ((size_t)(col / S) * H + row) * S + (col % S);
+}
+template <int R, int S>
+__global__ void __launch_bounds__(256) k_mimic_s(const cf* __restrict__ sp, const cf* __restrict__ uxi,
+                                                 const cf* __restrict__ uyi, const cf* __restrict__ b,
+                                                 cf* __restrict__ uxo, cf* __restrict__ uyo, cf* __restrict__ so,
+                                                 int H, long long nstrips) {
+    const int t = threadIdx.x % L;
+    const long long strip = (long long)blockIdx.x * 4 + threadIdx.x / L;
+    if (strip >= nstrips) return;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    const size_t base = (size_t)p * H * N;
+    cf acc[E];
+    for (int j = 0; j < E; ++j) acc[j] = ld(&sp[base + soff<S>(H, (i0 - 1 + H) & (H - 1), t + L * j)], true);
+    for (int rr = 0; rr <= R; ++rr) {
+        const int gi = (i0 + rr) & (H - 1), gm = (i0 + rr - 1 + H) & (H - 1);
+        const size_t ro = base + (size_t)gi * N;
+        const size_t rm = base + (size_t)gm * N;
+        cf x[E], uy[E];
+        for (int j = 0; j < E; ++j) x[j] = ld(&sp[base + soff<S>(H, gi, t + L * j)], true);
+        for (int j = 0; j < E; ++j) { uy[j] = ld(&uyi[ro + t + L * j], true); uy[j].x += x[j].x; uy[j].y += acc[j].y; }
+        if (rr < R) for (int j = 0; j < E; ++j) st(&uyo[ro + t + L * j], uy[j], true);
+        if (rr >= 1) {
+            for (int j = 0; j < E; ++j) { cf bb = ld(&b[rm + t + L * j], true); acc[j].x += bb.x; acc[j].y -= bb.y; }
+            for (int j = 0; j < E; ++j) st(&so[base + soff<S>(H, gm, t + L * j)], acc[j], true);
+        }
+        if (rr < R) {
+            for (int j = 0; j < E; ++j) { cf u = ld(&uxi[ro + t + L * j], true); u.x -= x[j].y; u.y += x[j].x; st(&uxo[ro + t + L * j], u, true); }
+        }
+        for (int j = 0; j < E; ++j) acc[j] = x[j];
+    }
+}
+// pass B on the strip layout: C columns x all H rows per block (C <= S), in place, optional XCD remap
+template <int C, int TPB, int S, bool REMAP>
+__global__ void __launch_bounds__(TPB) k_colmimic_s(cf* __restrict__ spec, int H, int colblocks) {
+    constexpr int LL = TPB / C;
+    const int c = threadIdx.x % C, t = threadIdx.x / C;
+    const unsigned lb = REMAP ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int p = lb / colblocks, cb = lb % colblocks;
+    cf* base = spec + (size_t)p * H * N;
+    const int EE = H / LL;
+    cf v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < EE) v[j] = base[soff<S>(H, t + LL * j, cb * C + c)];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) if (j < EE) { v[j].x *= 1.0001f; base[soff<S>(H, t + LL * j, cb * C + c)] = v[j]; }
+}
+
 int main() {
     const int P = 192, H = 1024;
     const size_t n = (size_t)P * H * N;  // cf per array
@@ -524,6 +577,24 @@ int main() {
         printf("%-40s %8.4f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
     const double arr = (double)n * sizeof(cf);
+    if (getenv("STRIP_SWEEP")) {
+        const long long ns = (long long)P * H / 8;
+        const int cb8 = N / 8;
+        for (int rep = 0; rep < 3; ++rep) {
+            timeit("A row-major nt (prod) R=8", 7 * arr, [&] { k_mimic<8, true, true><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A strips S=16 nt R=8", 7 * arr, [&] { k_mimic_s<8, 16><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A strips S=32 nt R=8", 7 * arr, [&] { k_mimic_s<8, 32><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("A strips S=64 nt R=8", 7 * arr, [&] { k_mimic_s<8, 64><<<(unsigned)((ns + 3) / 4), 256>>>(buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], H, ns); });
+            timeit("B row-major C=8 remap (prod)", 2 * arr, [&] { k_colmimic_mix<512, 8, false, false, true><<<(unsigned)(P * cb8), 512>>>(buf[6], buf[6], H, cb8); });
+            timeit("B strips16 C=8 remap", 2 * arr, [&] { k_colmimic_s<8, 512, 16, true><<<(unsigned)(P * cb8), 512>>>(buf[6], H, cb8); });
+            timeit("B strips16 C=8 noremap", 2 * arr, [&] { k_colmimic_s<8, 512, 16, false><<<(unsigned)(P * cb8), 512>>>(buf[6], H, cb8); });
+            timeit("B strips32 C=8 remap", 2 * arr, [&] { k_colmimic_s<8, 512, 32, true><<<(unsigned)(P * cb8), 512>>>(buf[6], H, cb8); });
+            timeit("B strips64 C=8 remap", 2 * arr, [&] { k_colmimic_s<8, 512, 64, true><<<(unsigned)(P * cb8), 512>>>(buf[6], H, cb8); });
+            timeit("B strips16 C=16 1024thr remap", 2 * arr, [&] { k_colmimic_s<16, 1024, 16, true><<<(unsigned)(P * cb8 / 2), 1024>>>(buf[6], H, cb8 / 2); });
+            timeit("copy float4", 2 * arr, [&] { k_copy<false><<<16384, 256>>>((const float4*)buf[0], (float4*)buf[1], arr / 16); });
+        }
+        return 0;
+    }
     if (getenv("U4_SWEEP")) {
         const long long ns = (long long)P * H / 8;
         for (int rep = 0; rep < 3; ++rep) {
