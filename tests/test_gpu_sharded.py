@@ -1,4 +1,4 @@
-"""Batch sharding on the GPU with world size 2 (two processes on cuda:0, gloo backend: RCCL refuses
+"""Batch sharding on the GPU with world sizes 2 and 8 (processes on cuda:0, gloo backend: RCCL refuses
 two ranks on one device; the 8-GPU RCCL run is the driver's).
 
 * aniso: no data-path collective; gathered output equals the single-process solve bit for bit
@@ -100,24 +100,30 @@ def _direct_iso(xl, k, lam, rho, maxit):
     return out
 
 
-@pytest.mark.parametrize("iso,B", [(False, 5), (True, 5), (True, 1)])
-def test_sharded_world2_on_gpu(cuda_dev, iso, B):
+@pytest.mark.parametrize("world,iso,B", [(2, False, 5), (2, True, 5), (2, True, 1), (8, False, 16), (8, True, 11)])
+def test_sharded_world2_on_gpu(cuda_dev, world, iso, B):
     """B = 1 with iso: rank 1's shard is empty and takes part in every all-reduce of the forward
-    and the backward with zeros (ABI v4 participate-only call); without that rank 0 would hang."""
+    and the backward with zeros (ABI v4 participate-only call); without that rank 0 would hang.
+    world = 8: config 4's topology (BASELINE configs[3]: the batch over 8 ranks, 64 images each),
+    here 16 images (2 per rank) and 11 (uneven shards: 2 2 2 1 1 1 1 1) at a reduced size."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, iso, q, B)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, iso, q, B)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    for rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat, e_side, e_direct in sorted(q.get(timeout=10) for _ in range(2)):
+    for rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat, e_side, e_direct in sorted(q.get(timeout=10) for _ in range(world)):
         print("iso" if iso else "aniso", rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat, e_side, e_direct)
         if iso:
             # fp32 reassociation only: per-pixel norms and tau^ partials summed per rank, then across
-            assert e_out <= 1e-6 and e_gx <= 1e-5 and e_gl <= 5e-5 and e_gr <= 1e-4 and e_gat <= 1e-6
+            # (the rho gradient is a small sum of cancelling per-strip partials: its relative error
+            # grows with the number of partial sums reassociated across ranks -- measured 2.2e-5 at 2
+            # ranks, 1.0e-4 at 8)
+            gr_gate = 1e-4 if world <= 2 else 4e-4
+            assert e_out <= 1e-6 and e_gx <= 1e-5 and e_gl <= 5e-5 and e_gr <= gr_gate and e_gat <= 1e-6
             # the same solve on a non-default torch stream, and on a library stream that is not torch's
             assert e_side <= 1e-6 and e_direct <= 1e-6
         else:
