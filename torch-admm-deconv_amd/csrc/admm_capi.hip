@@ -1167,6 +1167,14 @@ template <int S> int gcol_mm_launch(const GColMMArgs& a, size_t lds, hipStream_t
     hipLaunchKernelGGL(k_gcol_mm<S>, grid, dim3(256), lds, s, a);
     return launch_check("k_gcol_mm");
 }
+// phase skips of the matrix-core column pass for timing experiments (results invalid): only in a
+// library built with -DADMM_MM_DBG_BUILD=1 (tools/build_variant.sh), never from the environment of a
+// product build
+#ifndef ADMM_MM_DBG_BUILD
+#define ADMM_MM_DBG_BUILD 0
+#endif
+inline int mm_dbg() { return ADMM_MM_DBG_BUILD ? env_int("ADMM_MM_DBG", 0) : 0; }
+
 template <class T>
 int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx_t<T>* tw, int H, int W, long long P,
          int mode, hipStream_t s, cx_t<T>* gscr = nullptr) {
@@ -1175,7 +1183,7 @@ int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx
         if (mode == 0 && m.ok) {  // the factor's [H][Wh] copy follows fcT (setup, k_fc_transpose)
             const int Wh = W / 2 + 1;
             GColMMArgs a{spec, dump, fcT + (size_t)Wh * H, tw, H, m.R, m.h, m.KS, m.MT, m.NL, __builtin_ctz(m.NL), m.RP,
-                         Wh, (Wh + m.NL - 1) / m.NL, P, env_int("ADMM_MM_DBG", 0)};
+                         Wh, (Wh + m.NL - 1) / m.NL, P, mm_dbg()};
             switch (m.S) {
                 case 1: return gcol_mm_launch<1>(a, m.lds, s);
                 case 2: return gcol_mm_launch<2>(a, m.lds, s);
