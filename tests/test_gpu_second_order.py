@@ -82,3 +82,31 @@ def test_hessian_vector_product_module(cuda_dev):
     r0, eps = float(d["rho"][0]), 1e-6
     fd = (grad_lam(r0 + eps) - grad_lam(r0 - eps)) / (2 * eps)
     assert abs(float(hlr) - float(fd)) <= 1e-5 * max(1.0, abs(float(fd))), (float(hlr), float(fd))
+
+
+def test_grouped_modules_second_order(cuda_dev):
+    """fft_admm_tv_grouped (two modules sharing x, one native call) differentiates twice like the two
+    separate solves: a gradient penalty on x reaching both modules' lambda / rho."""
+    from admmtor.eops.deconv import fft_admm_tv, fft_admm_tv_grouped
+    from admmtor.synth import blurred_batch, make_psf
+    psf = make_psf("motion", 5).to(cuda_dev)
+    x0 = blurred_batch(2, 3, 32, 64, psf.cpu(), seed=4).to(cuda_dev)
+
+    def run(grouped):
+        x = x0.clone().requires_grad_(True)
+        lams = [torch.tensor([0.02], device=cuda_dev, requires_grad=True),
+                torch.tensor([0.01], device=cuda_dev, requires_grad=True)]
+        rhos = [torch.tensor([0.05], device=cuda_dev, requires_grad=True),
+                torch.tensor([0.04], device=cuda_dev, requires_grad=True)]
+        if grouped:
+            outs = fft_admm_tv_grouped(x, lams, rhos, psf, True, 6)
+        else:
+            outs = [fft_admm_tv(x, l, r, psf, True, 6) for l, r in zip(lams, rhos)]
+        loss = sum((o * o).sum() for o in outs)
+        (gx,) = torch.autograd.grad(loss, x, create_graph=True)
+        pen = (gx * gx).sum()
+        return torch.autograd.grad(pen, [x] + lams + rhos)
+
+    hg, hs = run(True), run(False)
+    for a, b in zip(hg, hs):
+        assert rel_l2(a.detach().cpu(), b.detach().cpu()) <= 1e-5

@@ -92,3 +92,16 @@ def test_oracle_second_order_matches_reference(tag):
     h = torch.autograd.grad(pen, (cot, x, lam, rho, k))
     for got, key in zip(h, ("hcot", "hx", "hlam", "hrho", "hpsf")):
         assert rel_l2(got, d[key]) <= 1e-10, key
+
+
+def test_unrolled_solve_grouped_modules():
+    """G modules sharing xin (fft_admm_tv_grouped's layout): module-major output, each module its own
+    lambda / rho and, with iso, its own norm over its (B, C) -- equal to the separate solves."""
+    d, psf, kgrad, iso, maxit, sl, sr = case("iso_psf")
+    lam = torch.tensor([0.02, 0.05], dtype=torch.float64)
+    rho = torch.tensor([0.05, 0.03], dtype=torch.float64)
+    both = unrolled_solve(d["x"], lam, rho, psf, True, maxit)
+    B = d["x"].shape[0]
+    for g in range(2):
+        one = unrolled_solve(d["x"], lam[g:g + 1], rho[g:g + 1], psf, True, maxit)
+        assert torch.equal(both[g * B:(g + 1) * B], one)
