@@ -365,10 +365,12 @@ template <int H, int C> int pass_b_hc(const cf* spec, cf* out, const float* fcT,
     const dim3 grid((unsigned)((long long)((P + gp - 1) / gp) * colblocks));
     const int order = gp > 1 ? 1 : passb_order(H);
     const int fpack = mode == 0 && env_int("ADMM_PASSB_FPACK", 1) ? 1 : 0;  // A/B knob
-    // block remap / plane order (k_pass_b pmode): contiguous XCD ranges, plane groups walked in
-    // reverse (the planes pass A wrote last first): pass B 0.3465 -> 0.3420 ms at C3, whole
-    // iteration +-0; pair-interleaved remap (4, 5) +9 % (profiles/r03_ab_passb_order.txt)
-    const int pmode = env_int("ADMM_PASSB_PMODE", 3);
+    // block remap / plane order (k_pass_b pmode): contiguous XCD ranges (2), plane groups walked
+    // forward; the reverse walk (3) takes pass B alone 0.3465 -> 0.3420 ms at C3 but the iteration is
+    // faster with the forward one (4 interleaved rounds: C3 706-722 -> 710-728 it/s, C2 5,572 ->
+    // 5,624, C3 iso +0.5 %; profiles/r03_sweep_knobs_c3.txt); pair-interleaved remap (4, 5) +9 %
+    // (profiles/r03_ab_passb_order.txt)
+    const int pmode = env_int("ADMM_PASSB_PMODE", 2);
     if (mode == 0) {
         if (int e = set_lds(k_pass_b<H, C, 0>, G::lds_bytes())) return e;
         hipLaunchKernelGGL((k_pass_b<H, C, 0>), grid, dim3(G::NT), G::lds_bytes(), s, spec, out, fcT, mT, twH, N, colblocks, ppm,
@@ -1479,7 +1481,10 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     // The inference path keeps its internal images (u, b, iso norm maps) in the lane-paired row
     // layout (16-byte accesses, admm_kernels.hpp ld_row); the training history stays in pixel order.
     // ADMM_PL=0 for the pixel-order layout (A/B).
-    const bool pl = !train && env_int("ADMM_PL", 1) != 0;
+    // Default on for iso (C3 iso 507-514 -> 533-544 it/s) and rows up to 512 (C2 +1 %), off for aniso
+    // rows of 1,024+ where the pixel-order streams measured faster (C3 pass A 1.0355 -> 1.0295 ms, 4
+    // interleaved rounds, profiles/r03_sweep_knobs_c3.txt).
+    const bool pl = !train && env_int("ADMM_PL", (d.iso || W < 1024) ? 1 : 0) != 0;
 
     // b = H_t(xin) once (the reference recomputes it every iteration, deconv.py:104)
     const float* bimg = xin;
