@@ -41,6 +41,8 @@ CONFIGS = {
               "C3 with block (iso) shrinkage, the ADMMDeconv default: batch-64 1024x1024x3, 21x21 PSF, 50 iters"),
     "bsd": (32, 3, 321, 481, "gauss:1.5", 9, 50, False,
             "generic-size path (row f4): batch-32 481x321x3 (BSD image size), 9x9 Gaussian PSF, aniso, 50 iters"),
+    "hd": (8, 3, 1080, 1920, "gauss:1.5", 9, 50, False,
+           "generic-size path (row f4): batch-8 1080x1920x3 (HD frame), 9x9 Gaussian PSF, aniso, 50 iters"),
     "c2": (32, 3, 512, 512, "motion", 15, 50, False,
            "C2: batch-32 512x512x3, 15x15 motion PSF, lambda 0.01, rho 0.02, aniso, 50 iters"),
     "c5fwd": (16, 3, 512, 512, "none", 0, 100, True,
@@ -60,6 +62,10 @@ ISO_NORM_BYTES = 12
 # generic sizes: the column pass (half spectra in and out, 8) and the inverse row transform that
 # follows it in the same timer (half spectra in 4, x image out 4)
 GEN_COL_BYTES = 16
+# training backward, reverse row pass (admm_backward.hpp k_bwd_pass_a) per reverse step k: reads the
+# r^ spectrum 4, a^_k 8, a_k 8, a_{k-1} 8, b^ 4; writes b^ 4, a^_{k-1} 8, the x^ spectrum 4 = 48;
+# k = K reads no a^ and no b^ (36); k = 1 reads no a_{k-1} and writes no a^ / x^ (28)
+BWD_ROW_BYTES, BWD_ROW_LAST_BYTES, BWD_ROW_FIRST_BYTES = 48, 36, 28
 
 
 def parse():
@@ -71,7 +77,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
-                    help="c3: skip the extra C3-at-100-iterations and C3-iso measurements after the timed region")
+                    help="c3: skip the extra measurements after the timed region (C3 at 100 iterations, C3 iso, "
+                         "the generic-size bsd / hd workloads, the training step)")
     ap.add_argument("--cpu-planes", type=int, default=6, help="CPU baseline sample: planes of 1024^2")
     ap.add_argument("--cpu-iters", type=int, default=36, help="CPU baseline sample: timed iterations")
     ap.add_argument("--c5-batch", type=int, default=None, help="C5 only: override the per-GPU batch")
@@ -135,6 +142,124 @@ def c3_extras(x, psf, lam, rho, no_parity, steps=3):
             e["rel_l2_vs"] = "fp64 CPU oracle, plane (0,0)"
         out[key] = e
     return out
+
+
+def generic_extras(dev, no_parity, keys=("bsd", "hd")):
+    """Generic-size path figures on the default line: for each workload one warm-up
+    solve, then timed solves on the default two-stream schedule (iterations/s, us per iteration per
+    Mpx), the rel-L2 of plane (0, 0) vs the fp64 oracle, and a one-stream profiling pass (ADMM_GEN_STREAMS=1:
+    the two streams' launches overlap) for the per-kernel achieved GB/s of the algorithmic bytes."""
+    from admmtor import _native
+    from admmtor.eops.deconv import fft_admm_tv
+    from admmtor.synth import CONFIG_SEED, blurred_batch, make_psf
+    out = {}
+    for key in keys:
+        B, C, H, W, kind, k, maxit, iso, desc = CONFIGS[key]
+        psf = make_psf(kind, k).to(dev)
+        x = blurred_batch(B, C, H, W, psf.cpu(), seed=CONFIG_SEED + 10, device=dev)
+        lam = torch.tensor([0.01], device=dev)
+        rho = torch.tensor([0.02], device=dev)
+        o = fft_admm_tv(x, lam, rho, psf, iso, maxit)
+        torch.cuda.synchronize()
+        steps = 10 if B * C * H * W < 20e6 else 4
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            o = fft_admm_tv(x, lam, rho, psf, iso, maxit)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        npx = B * C * H * W
+        e = {"value": maxit / dt, "unit": "iterations/s", "ms_per_step": dt * 1e3, "steps": steps,
+             "us_per_iter_per_Mpx": dt / maxit / (npx / 1e6) * 1e6, "workload": desc,
+             "path": "fused" if _native.load().admm_tv_supported(H, W) == 1 else "generic"}
+        if not no_parity:
+            from oracle.admm_oracle import rel_l2, solve_fourier
+            ref = solve_fourier(x[:1, :1].double().cpu(), 0.01, 0.02, psf.double().cpu(), iso, maxit)
+            e["rel_l2"] = rel_l2(o[:1, :1].cpu(), ref)
+            e["rel_l2_vs"] = "fp64 CPU oracle, plane (0,0)"
+        old = os.environ.get("ADMM_GEN_STREAMS")
+        os.environ["ADMM_GEN_STREAMS"] = "1"
+        try:
+            _native.profile_reset()
+            _native.profile_enable(True)
+            for _ in range(2):
+                fft_admm_tv(x, lam, rho, psf, iso, maxit)
+            torch.cuda.synchronize()
+            _native.profile_enable(False)
+            ms, cnt = _native.profile_read()
+        finally:
+            if old is None:
+                del os.environ["ADMM_GEN_STREAMS"]
+            else:
+                os.environ["ADMM_GEN_STREAMS"] = old
+        generic = e["path"] == "generic"
+        ba = (2 * PASS_A_FIRST_BYTES + (cnt[0] - 2) * PASS_A_BYTES) * npx
+        bb = cnt[1] * (GEN_COL_BYTES if generic else PASS_B_BYTES) * npx
+        per = {}
+        for name, t, n, b in (("row_step" if generic else "pass_a", ms[0], cnt[0], ba),
+                              ("column_pass" if generic else "pass_b", ms[1], cnt[1], bb)):
+            gbs = b / (t / 1e3) / 1e9 if t > 0 else None
+            per[name] = {"avg_launch_ms": t / max(n, 1), "launches": n, "algorithmic_bytes_per_launch": b / max(n, 1),
+                         "GBps": gbs, "frac": gbs / HBM_PEAK_GBS if gbs else None}
+        e["roofline_one_stream"] = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "per_kernel": per,
+                                    "timing": "HIP events, 2 solves on one stream after the timed solves"}
+        out[key] = e
+        del x, o
+    return out
+
+
+def train_extra(dev, steps=3):
+    """The training path (BASELINE configs[4]: autograd through the HIP op; reference: plain autograd
+    through deconv.py:103-115): one ADMMDeconv module at the C5 shape (batch-16 512x512x3, iso, no PSF,
+    100 iterations, learnable lambda / rho, seeded init), forward with history (admm_tv_forward_train) +
+    backward (admm_tv_backward) per step, timed with HIP events on torch's stream (where the op launches);
+    the reverse row pass's achieved GB/s from the library's per-launch events against its algorithmic
+    bytes (BWD_ROW_*)."""
+    from admmtor import _native
+    from admmtor.elayers.admmdeconv import ADMMDeconv
+    from admmtor.synth import CONFIG_SEED, blurred_batch
+    B, C, H, W, K = 16, 3, 512, 512, 100
+    torch.manual_seed(CONFIG_SEED + 5)
+    m = ADMMDeconv((), max_iters=K, iso=True).to(dev)
+    x = blurred_batch(B, C, H, W, torch.empty(0), seed=CONFIG_SEED + 5, device=dev).requires_grad_(True)
+    v = torch.randn(x.shape, generator=torch.Generator(device=dev).manual_seed(3), device=dev)
+    fwd_ms, bwd_ms = [], []
+    prof = None
+    for i in range(1 + steps):
+        m.zero_grad(set_to_none=True)
+        x.grad = None
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        out = m(x)
+        loss = (out * v).sum()
+        e1.record()
+        if i == steps:  # the last step's backward with the library's per-launch events
+            _native.profile_reset()
+            _native.profile_enable(True)
+        loss.backward()
+        e2.record()
+        torch.cuda.synchronize()
+        if i == steps:
+            _native.profile_enable(False)
+            prof = _native.profile_read()
+        if i > 0:
+            fwd_ms.append(e0.elapsed_time(e1))
+            bwd_ms.append(e1.elapsed_time(e2))
+    ms, cnt = prof
+    npx = B * C * H * W
+    nrow = cnt[0]
+    brow = ((nrow - 2) * BWD_ROW_BYTES + BWD_ROW_LAST_BYTES + BWD_ROW_FIRST_BYTES) * npx if nrow >= 2 else 0
+    gbs = brow / (ms[0] / 1e3) / 1e9 if ms[0] > 0 else None
+    f, b = sum(fwd_ms) / steps, sum(bwd_ms) / steps
+    return {"train": {"workload": "one ADMMDeconv module at the C5 shape: batch-16 512x512x3, iso, no PSF, 100 iters, "
+                                  "learnable lambda/rho, fp32 solve; forward with history + backward",
+                      "ms_per_step": f + b, "fwd_train_ms": f, "bwd_ms": b, "steps": steps,
+                      "steps_per_s": 1e3 / (f + b),
+                      "bwd_row_pass": {"avg_launch_ms": ms[0] / max(nrow, 1), "launches": nrow,
+                                       "algorithmic_bytes_per_launch": brow / max(nrow, 1), "GBps": gbs,
+                                       "frac": gbs / HBM_PEAK_GBS if gbs else None, "bound": "hbm"},
+                      "bwd_kernel_ms": {"row_pass": ms[0], "column_pass": ms[1], "iso_q": ms[2]},
+                      "grads_finite": bool(torch.isfinite(x.grad).all() and torch.isfinite(m.lmbda.grad).all()
+                                           and torch.isfinite(m.rho.grad).all())}}
 
 
 def cpu_baseline(cfg, planes, iters):
@@ -442,19 +567,23 @@ def main():
     achieved = (dbytes / (dms / 1e3)) / 1e9 if dms > 0 else 0.0
 
     traffic, traffic_src = pmc_traffic(args.config, dom, dn, roof_steps, build_hash)
+    parity = None
+    if rank == 0 and not args.no_parity:
+        from oracle.admm_oracle import rel_l2, solve_fourier
+        ref = solve_fourier(x[:1, :1].double().cpu(), 0.01, 0.02, psf.double().cpu(), iso, maxit) \
+            if not iso else None
+        if ref is not None:
+            parity = {"rel_l2": rel_l2(out[:1, :1].cpu(), ref),
+                      "vs": "fp64 CPU oracle (pinned to the reference), plane (0,0) of the last step"}
     extras = {}
     if rank == 0 and world == 1 and args.config == "c3" and not args.no_extras:
         extras = c3_extras(x, psf, lam, rho, args.no_parity)
+        del out, x  # free the C3 batch before the other workloads
+        torch.cuda.empty_cache()
+        extras.update(generic_extras(dev, args.no_parity))
+        extras.update(train_extra(dev))
     result = None
     if rank == 0:
-        parity = None
-        if not args.no_parity:
-            from oracle.admm_oracle import rel_l2, solve_fourier
-            ref = solve_fourier(x[:1, :1].double().cpu(), 0.01, 0.02, psf.double().cpu(), iso, maxit) \
-                if not iso else None
-            if ref is not None:
-                parity = {"rel_l2": rel_l2(out[:1, :1].cpu(), ref),
-                          "vs": "fp64 CPU oracle (pinned to the reference), plane (0,0) of the last step"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg, args.cpu_planes, args.cpu_iters)

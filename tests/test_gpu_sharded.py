@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, iso, q, B=5):
+def _worker(rank, world, port, iso, q, B=5, dt=torch.float32):
     import sys
     import torch.distributed as dist
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -38,17 +38,18 @@ def _worker(rank, world, port, iso, q, B=5):
         k = make_psf("motion", 7).to(dev)
         full = blurred_batch(B, 3, 64, 128, k.cpu(), seed=21).to(dev)
         cot = torch.randn(full.shape, generator=torch.Generator().manual_seed(5)).to(dev)
+        k, full, cot = k.to(dt), full.to(dt), cot.to(dt)
         s, e = shard_bounds(B, world, rank)
         # reference: single-process solve of the whole batch (+ gradients)
         xr = full.clone().requires_grad_(True)
-        lr = torch.tensor([0.02], device=dev, requires_grad=True)
-        rr = torch.tensor([0.05], device=dev, requires_grad=True)
+        lr = torch.tensor([0.02], device=dev, dtype=dt, requires_grad=True)
+        rr = torch.tensor([0.05], device=dev, dtype=dt, requires_grad=True)
         ref = fft_admm_tv(xr, lr, rr, k, iso, 15)
         (ref * cot).sum().backward()
         # sharded
         xs = full[s:e].clone().requires_grad_(True)
-        ls = torch.tensor([0.02], device=dev, requires_grad=True)
-        rs = torch.tensor([0.05], device=dev, requires_grad=True)
+        ls = torch.tensor([0.02], device=dev, dtype=dt, requires_grad=True)
+        rs = torch.tensor([0.05], device=dev, dtype=dt, requires_grad=True)
         out = sharded_fft_admm_tv(xs, ls, rs, k, iso, 15)
         (out * cot[s:e]).sum().backward()
         g = torch.cat([ls.grad, rs.grad])
@@ -59,7 +60,7 @@ def _worker(rank, world, port, iso, q, B=5):
             return ((a.double() - b.double()).norm() / b.double().norm()).item() if b.numel() else 0.0
 
         side_rel = direct_rel = 0.0
-        if iso:
+        if iso and dt == torch.float32:
             # (a) the sharded solve inside a non-default torch stream
             st = torch.cuda.Stream(dev)
             st.wait_stream(torch.cuda.current_stream(dev))
@@ -100,8 +101,30 @@ def _direct_iso(xl, k, lam, rho, maxit):
     return out
 
 
-@pytest.mark.parametrize("world,iso,B", [(2, False, 5), (2, True, 5), (2, True, 1), (8, False, 16), (8, True, 11)])
-def test_sharded_world2_on_gpu(cuda_dev, world, iso, B):
+def _rho_grad_noise(B):
+    """How far the reference formulation's fp32 rho gradient sits from its fp64 one on this test's
+    input (fp32 vs fp64 autograd through the oracle's restatement, CPU).  The rho gradient of this
+    iso solve is ill-conditioned: a 1e-7 relative perturbation of the per-pixel norm sums alone moves
+    it by ~1.4e-4, so the fp32 reassociation of those sums across ranks cannot be held
+    to a fixed 1e-4; the gate is this measured noise floor instead (the fp64 runs below show the
+    sharding itself is exact to ~1e-12)."""
+    from admmtor.synth import blurred_batch, make_psf
+    from oracle.admm_oracle import solve_fourier
+    k = make_psf("motion", 7)
+    full = blurred_batch(B, 3, 64, 128, k, seed=21)
+    cot = torch.randn(full.shape, generator=torch.Generator().manual_seed(5))
+    g = []
+    for dt in (torch.float32, torch.float64):
+        lam = torch.tensor([0.02], dtype=dt, requires_grad=True)
+        rho = torch.tensor([0.05], dtype=dt, requires_grad=True)
+        out = solve_fourier(full.to(dt), lam, rho, k.to(dt), True, 15)
+        g.append(torch.autograd.grad((out * cot.to(dt)).sum(), rho)[0].double().item())
+    return abs(g[0] - g[1]) / abs(g[1])
+
+
+@pytest.mark.parametrize("world,iso,B,f64", [(2, False, 5, False), (2, True, 5, False), (2, True, 1, False),
+                                             (8, False, 16, False), (8, True, 11, False), (8, True, 11, True)])
+def test_sharded_world2_on_gpu(cuda_dev, world, iso, B, f64):
     """B = 1 with iso: rank 1's shard is empty and takes part in every all-reduce of the forward
     and the backward with zeros (ABI v4 participate-only call); without that rank 0 would hang.
     world = 8: config 4's topology (BASELINE configs[3]: the batch over 8 ranks, 64 images each),
@@ -109,20 +132,27 @@ def test_sharded_world2_on_gpu(cuda_dev, world, iso, B):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, iso, q, B)) for r in range(world)]
+    dt = torch.float64 if f64 else torch.float32
+    procs = [ctx.Process(target=_worker, args=(r, world, port, iso, q, B, dt)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    noise = _rho_grad_noise(B) if (iso and not f64) else 0.0
+    if noise:
+        print(f"reference-formulation fp32 rho-gradient noise on this input: {noise:.2e}")
     for rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat, e_side, e_direct in sorted(q.get(timeout=10) for _ in range(world)):
         print("iso" if iso else "aniso", rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat, e_side, e_direct)
-        if iso:
-            # fp32 reassociation only: per-pixel norms and tau^ partials summed per rank, then across
-            # (the rho gradient is a small sum of cancelling per-strip partials: its relative error
-            # grows with the number of partial sums reassociated across ranks -- measured 2.2e-5 at 2
-            # ranks, 1.0e-4 at 8)
-            gr_gate = 1e-4 if world <= 2 else 4e-4
+        if iso and f64:
+            # fp64: the sharded solve is the single-process one up to fp64 reassociation of the
+            # per-pixel sums -- the machinery adds no error of its own
+            assert e_out <= 1e-12 and e_gx <= 1e-11 and e_gl <= 1e-10 and e_gr <= 1e-9 and e_gat <= 1e-12
+        elif iso:
+            # fp32 reassociation only: per-pixel norms and Q summed per rank, then across.  The rho
+            # gradient's gate is the reference formulation's own fp32 noise on this input (measured
+            # 2.2e-4; sharded: 2.2e-5 at 2 ranks, 1.0e-4 at 8), at least 1e-4
+            gr_gate = max(1e-4, noise)
             assert e_out <= 1e-6 and e_gx <= 1e-5 and e_gl <= 5e-5 and e_gr <= gr_gate and e_gat <= 1e-6
             # the same solve on a non-default torch stream, and on a library stream that is not torch's
             assert e_side <= 1e-6 and e_direct <= 1e-6

@@ -141,3 +141,45 @@ def test_shard_bounds_cover_exactly():
             assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
             sizes = [e - s for s, e in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _subgroup_worker(rank, world, port, q):
+    """A subgroup's host group is created by its members only (use_local_synchronization): rank 2,
+    outside the subgroup, never enters, and ranks 0 and 1 must not wait for it."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "torch-admm-deconv_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from admmtor import sharded
+        sub = dist.new_group(ranks=[0, 1])  # a collective over the whole world, as torch requires
+        res = None
+        if rank in (0, 1):
+            hg = sharded.make_host_group(sub)
+            assert sharded.make_host_group(sub) is hg                    # cached per rank set
+            assert sharded._group_key(sub) == (0, 1)
+            assert sharded._group_key(None) == (0, 1, 2)
+            t = torch.tensor([10 + rank], dtype=torch.int64)
+            parts = [torch.zeros(1, dtype=torch.int64) for _ in range(2)]
+            dist.all_gather(parts, t, group=hg)
+            res = [int(p[0]) for p in parts]
+        q.put((rank, res))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_group_of_a_subgroup_world3():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = dict(q.get(timeout=5) for _ in range(world))
+    assert res == {0: [10, 11], 1: [10, 11], 2: None}

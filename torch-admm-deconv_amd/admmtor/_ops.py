@@ -184,9 +184,14 @@ def _setup_context(ctx, inputs, output):
     x, lam, rho, kern, iso, maxit, psf_grad = inputs
     _, hist = output
     ctx.iso, ctx.maxit, ctx.psf_grad = iso, maxit, psf_grad
-    # x: read by the native backward only for the PSF gradient (b = H_t(x) path); kept in every case
-    # for a double backward (a reference to the input, no copy)
-    ctx.save_for_backward(x, lam, rho, kern, hist)
+    # x: read by the native backward only for the PSF gradient (b = H_t(x) path), and by a double
+    # backward (admmtor._unrolled rebuilds the iteration from it).  An x that requires grad is saved
+    # as itself (the double backward must reach it; autograd's usual version check applies, as for
+    # any op that saves its input).  Otherwise a private copy is kept: the reference's graph saves no
+    # reference to xin (its circular pad copies), so a caller may still modify xin in place after
+    # the forward and call backward (one image of memory next to the 2 K images of history).
+    xs = x if x.requires_grad else x.detach().clone()
+    ctx.save_for_backward(xs, lam, rho, kern, hist)
 
 
 def _backward(ctx, gout, ghist):

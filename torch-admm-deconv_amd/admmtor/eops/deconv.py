@@ -183,6 +183,24 @@ def fft_admm_tv(xin: torch.Tensor,
     return _fft_admm_tv_impl(xin, lmbd, rho, kern, iso, maxit)
 
 
+# A line whose length has a prime factor R beyond Bluestein's reach (2R - 1 > 1024, or any R on lines
+# longer than 10,240 points) runs that factor as an any-prime stage: every output a sum of R terms, O(R)
+# per output.  In fp32 those sums lose accuracy as R grows (13,001: 7.1e-6 vs the fp64 oracle, the 1e-5
+# gate close); fp32 solves with a prime factor above this bound therefore compute in fp64 (the generic
+# kernels' double instantiation) and return fp32 -- same kernels, same cost order (O(n R) per line),
+# fp64 accuracy.  tests/test_gpu_generic.py runs 65,521, the largest prime line accepted.
+F32_MAX_PRIME = 16384
+
+
+def _largest_prime(n: int) -> int:
+    big, f = 1, 2
+    while f * f <= n:
+        while n % f == 0:
+            big, n = f, n // f
+        f += 1
+    return max(big, n)
+
+
 def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> torch.Tensor:
     """fft_admm_tv with an optional cross-rank all-reduce hook (admmtor.sharded)."""
     if not isinstance(kern, torch.Tensor):
@@ -190,6 +208,8 @@ def _fft_admm_tv_impl(xin, lmbd, rho, kern, iso=False, maxit=100, hook=None) -> 
     _check_inputs(xin, kern)
     home, out_dtype = xin.device, (torch.float64 if xin.dtype == torch.float64 else torch.float32)
     cdt = out_dtype  # the solve's arithmetic: fp64 for fp64 inputs, else fp32
+    if cdt == torch.float32 and max(_largest_prime(int(xin.shape[2])), _largest_prime(int(xin.shape[3]))) > F32_MAX_PRIME:
+        cdt = torch.float64  # see F32_MAX_PRIME
     maxit = max(0, int(maxit))  # the reference loops over torch.arange(0, maxit): negative -> no iteration
     # empty batch: the reference's ops return an empty result of the same shape.  An empty shard of
     # an iso solve over ranks still runs: it must take part in every iteration's all-reduce.

@@ -20,7 +20,20 @@ from typing import Callable, Optional
 import torch
 import torch.distributed as dist
 
-__all__ = ["shard_bounds", "broadcast_params", "sharded_fft_admm_tv"]
+__all__ = ["shard_bounds", "broadcast_params", "sharded_fft_admm_tv", "make_host_group"]
+
+# Test-only switch: run every collective of the sharded path (the parameter broadcast, the iso
+# all-reduce hook, the output gather) also at world size 1, where they are identities -- so a
+# single-GPU box can execute the RCCL calls of the multi-GPU path (tests/test_gpu_c4.py).
+_FORCE_COLLECTIVES = False
+
+
+def _world(group) -> int:
+    return dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+
+
+def _collectives(group) -> bool:
+    return _world(group) > 1 or (_FORCE_COLLECTIVES and dist.is_available() and dist.is_initialized())
 
 
 def shard_bounds(total: int, world: int, rank: int):
@@ -55,7 +68,7 @@ def broadcast_params(kern: torch.Tensor, lmbd, rho, group=None, src: int = 0, de
                                       if kern.numel() else torch.empty(0, device=device))
     lam = lmbd if trainable(lmbd) else _as_tensor(lmbd, device)
     rh = rho if trainable(rho) else _as_tensor(rho, device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _collectives(group):
         parts = [t for t in (lam, rh, k) if not trainable(t)]
         if parts:
             packed = torch.cat([t.reshape(-1).to(torch.float64) for t in parts])  # one collective, exact
@@ -83,17 +96,18 @@ def sharded_fft_admm_tv(x_local: torch.Tensor, lmbd, rho, kern: torch.Tensor, is
                  to equal size internally)
     solver       defaults to admmtor.eops.deconv.fft_admm_tv (the HIP path)
     """
-    world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+    world = _world(group)
+    coll = _collectives(group)
     if solver is None:
         from admmtor import _native
         from admmtor.eops.deconv import _fft_admm_tv_impl
-        hook = _native.AllReduceHook(group) if (iso and world > 1) else None
+        hook = _native.AllReduceHook(group) if (iso and coll) else None
 
         def solver(x, l, r, k, i, m):
             return _fft_admm_tv_impl(x, l, r, k, i, m, hook=hook)
     k, lam, rh = broadcast_params(kern, lmbd, rho, group=group, device=x_local.device)
     out = solver(x_local, lam, rh, k, iso, maxit)
-    if gather is None or world == 1:
+    if gather is None or not coll:
         return out
     if gather != "all":
         raise ValueError("gather must be None or 'all'")
@@ -117,19 +131,35 @@ def sharded_fft_admm_tv(x_local: torch.Tensor, lmbd, rho, kern: torch.Tensor, is
 _size_groups = {}
 
 
+def _group_key(group):
+    """Cache key of a process group: its global ranks (an ``id()`` can be reused by a later group
+    after the first is garbage-collected, which would hand back a gloo group over other ranks)."""
+    return tuple(range(dist.get_world_size())) if group is None else tuple(dist.get_process_group_ranks(group))
+
+
+def make_host_group(group=None):
+    """The CPU (gloo) group over the ranks of `group` that ``shard_sizes`` exchanges sizes on.
+
+    Created with ``use_local_synchronization=True``: only the member ranks of `group` enter the
+    creation (``new_group`` is otherwise a collective over the whole default world, so a subgroup's
+    first gather would hang waiting for the ranks outside it).  Cached per rank set.  Callers that
+    prefer to build it up front (e.g. right after creating `group`, on its members) may call this
+    once; ``shard_sizes`` otherwise creates it on first use."""
+    key = _group_key(group)
+    if key not in _size_groups:
+        ranks = None if group is None else list(key)
+        _size_groups[key] = dist.new_group(ranks=ranks, backend="gloo", use_local_synchronization=True)
+    return _size_groups[key]
+
+
 def _host_group(group):
     """A CPU (gloo) process group over the same ranks as `group`, for host-side metadata: exchanging
     shard sizes there needs no device synchronisation (an RCCL collective of a size tensor would
     need a .item() host sync, which breaks the no-sync / graph-capturable contract of b3/b5).
-    Created once per group, collectively, on first use (every rank reaches it through the same
-    sharded_fft_admm_tv call)."""
+    A gloo `group` is used as it is; for any other backend see ``make_host_group``."""
     if dist.get_backend(group) == "gloo":
         return group
-    key = id(group) if group is not None else None
-    if key not in _size_groups:
-        ranks = None if group is None else dist.get_process_group_ranks(group)
-        _size_groups[key] = dist.new_group(ranks=ranks, backend="gloo")
-    return _size_groups[key]
+    return make_host_group(group)
 
 
 def shard_sizes(local: int, group=None, total_batch: Optional[int] = None):

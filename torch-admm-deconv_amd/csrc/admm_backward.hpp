@@ -38,7 +38,7 @@ struct BwdArgs {
     const float* qp;      // iso: Q_{k-1} = sum_{b,c} a_{k-1} z^_{k-1}          [2][H][W]
     const float* lam;
     const float* rho;
-    float* part;          // per strip: {rho^ partial, tau^ partial}            [nstrips][2]
+    double* part;         // per strip: {rho^ partial, tau^ partial}, fp64      [nstrips][2]
     const cf* twW;
     int H, R;
     long long nstrips;
@@ -129,7 +129,9 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
     const cf* qpx = reinterpret_cast<const cf*>(a.qp + moff);
     const cf* qpy = reinterpret_cast<const cf*>(a.qp + moff + (size_t)H * W);
 
-    float rho_acc = 0.f, tau_acc = 0.f;
+    // the lambda / rho gradient partials accumulate in fp64 from the first product on (per lane,
+    // then over the sub-group, the strips and the iterations: k_bwd_scalars)
+    double rho_acc = 0.0, tau_acc = 0.0;
     cf rprev[E], rcur[E], abxp[E], abyp[E];
     {
         const int g = (i0 - 1 + H) & (H - 1);
@@ -163,7 +165,7 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
                     const cf ak = ld_pol<kNT>(&aky[i]);
                     const float e0 = (2.f * zp0 - ap.x) - (ak.x - ap.x + zp0);
                     const float e1 = (2.f * zp1 - ap.y) - (ak.y - ap.y + zp1);
-                    rho_acc = fmaf(d0, e0, fmaf(d1, e1, rho_acc));
+                    rho_acc = fma((double)d0, (double)e0, fma((double)d1, (double)e1, rho_acc));
                 }
                 if constexpr (!FIRSTK) {
                     const cf ub = LASTK ? mkc(0.f, 0.f) : ld_pol<kNT>(&abyi[i]);
@@ -174,7 +176,7 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
                     abyc[j] = mkc(ub.x - wb0 + shrink_vjp<ISO>(ap.x, zb0, tau, npv.x, q.x),
                                   ub.y - wb1 + shrink_vjp<ISO>(ap.y, zb1, tau, npv.y, q.y));
                     if constexpr (!ISO) {
-                        if (rr < R) tau_acc += soft_dtau(ap.x, zb0, tau) + soft_dtau(ap.y, zb1, tau);
+                        if (rr < R) tau_acc += (double)soft_dtau(ap.x, zb0, tau) + (double)soft_dtau(ap.y, zb1, tau);
                     }
                 }
             }
@@ -236,7 +238,7 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
                 const cf ak = ld_pol<kNT>(&akx[i]);
                 const float e0 = (2.f * zp0 - ap.x) - (ak.x - ap.x + zp0);
                 const float e1 = (2.f * zp1 - ap.y) - (ak.y - ap.y + zp1);
-                rho_acc = fmaf(d0, e0, fmaf(d1, e1, rho_acc));
+                rho_acc = fma((double)d0, (double)e0, fma((double)d1, (double)e1, rho_acc));
                 if constexpr (!FIRSTK) {
                     const cf ub = LASTK ? mkc(0.f, 0.f) : ld_pol<kNT>(&abxi[i]);
                     const float wb0 = rho * d0, wb1 = rho * d1;
@@ -245,7 +247,7 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
                     if constexpr (ISO) q = qpx[i];
                     abxp[j] = mkc(ub.x - wb0 + shrink_vjp<ISO>(ap.x, zb0, tau, npv.x, q.x),
                                   ub.y - wb1 + shrink_vjp<ISO>(ap.y, zb1, tau, npv.y, q.y));
-                    if constexpr (!ISO) tau_acc += soft_dtau(ap.x, zb0, tau) + soft_dtau(ap.y, zb1, tau);
+                    if constexpr (!ISO) tau_acc += (double)soft_dtau(ap.x, zb0, tau) + (double)soft_dtau(ap.y, zb1, tau);
                 }
             }
             if constexpr (!FIRSTK) {
@@ -353,14 +355,14 @@ __global__ void __launch_bounds__(256) k_bwd_iso_q(BwdIsoArgs a) {
 // one partial per block, fixed order.
 template <class T = float>
 __global__ void k_iso_tau_partial(const T* __restrict__ q, const T* __restrict__ n, const T* __restrict__ lam,
-                                  const T* __restrict__ rho, T* __restrict__ part, long long count) {
-    __shared__ T red[256];
+                                  const T* __restrict__ rho, double* __restrict__ part, long long count) {
+    __shared__ double red[256];
     const T tau = lam[0] / rho[0];
-    T acc = 0;
+    double acc = 0.0;  // fp64 from the first term (each term is the solve's precision)
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count;
          i += (long long)gridDim.x * blockDim.x) {
         const T s = sqrt(n[i] + eps15<T>()), d = s + eps15<T>();
-        if (T(1) - tau / d > T(0)) acc += -q[i] / d;
+        if (T(1) - tau / d > T(0)) acc += (double)(-q[i] / d);
     }
     red[threadIdx.x] = acc;
     __syncthreads();
@@ -375,19 +377,19 @@ __global__ void k_iso_tau_partial(const T* __restrict__ q, const T* __restrict__
 // lam^ = tau^ / rho.  part: [K][nstrips][2], the module's strips at [soff, soff + spm) of every
 // iteration; tpart (iso, or null): [K][G][ntp].  Single block, fixed order -> deterministic.
 template <class T = float>
-__global__ void k_bwd_scalars(const T* __restrict__ part, int K, long long nstrips, long long spm, long long soff,
-                              const T* __restrict__ tpart, int ntp, int G, int g, const T* __restrict__ lam,
+__global__ void k_bwd_scalars(const double* __restrict__ part, int K, long long nstrips, long long spm, long long soff,
+                              const double* __restrict__ tpart, int ntp, int G, int g, const T* __restrict__ lam,
                               const T* __restrict__ rho, T* __restrict__ glam, T* __restrict__ grho) {
     __shared__ double r1[256], r2[256];
     double sr = 0.0, st = 0.0;
     for (int it = 0; it < K; ++it) {
-        const T* pp = part + ((size_t)it * nstrips + soff) * 2;
+        const double* pp = part + ((size_t)it * nstrips + soff) * 2;
         for (long long i = threadIdx.x; i < spm; i += blockDim.x) {
             sr += pp[2 * i + 0];
             st += pp[2 * i + 1];
         }
         if (tpart) {
-            const T* tp = tpart + ((size_t)it * G + g) * ntp;
+            const double* tp = tpart + ((size_t)it * G + g) * ntp;
             for (int i = threadIdx.x; i < ntp; i += blockDim.x) st += tp[i];
         }
     }
@@ -422,31 +424,6 @@ __global__ void k_sum_modules(const float4* __restrict__ in, float4* __restrict_
         s.w += q.w;
     }
     out[i] = s;
-}
-
-// accumulate per-iteration scalar partials into a running [2] (rho^, tau^) pair in fp64-free fixed order
-__global__ void k_accum_parts(const float* __restrict__ part, long long n, float* __restrict__ acc) {
-    // acc[0..1] += sum(part[2i], part[2i+1]); one block
-    __shared__ float r1[256], r2[256];
-    float sr = 0.f, st = 0.f;
-    for (long long i = threadIdx.x; i < n; i += blockDim.x) {
-        sr += part[2 * i];
-        st += part[2 * i + 1];
-    }
-    r1[threadIdx.x] = sr;
-    r2[threadIdx.x] = st;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            r1[threadIdx.x] += r1[threadIdx.x + o];
-            r2[threadIdx.x] += r2[threadIdx.x + o];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        acc[0] += r1[0];
-        acc[1] += r2[0];
-    }
 }
 
 }  // namespace admm

@@ -136,6 +136,9 @@ size_t up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Layout {
     size_t spec[2], u[4], b, fcT, mT, twW, twH, twHd, G, part, nsq, sigma, total;
+    // generic path: the matrix-core plans, decided once per call (their environment knobs are read
+    // here only, so the regions sized below and the kernels launched later always agree)
+    MMPlan mm, mmr;
     size_t rimg;  // generic path: spec[0] = half spectra [P][H][W/2+1], spec[1] = x image, rimg = r image
     size_t gscr;  // generic path, lines beyond the LDS image: the transform blocks' scratch slots
     int ngroups, ppg;
@@ -158,6 +161,10 @@ Layout make_layout(const admm_tv_desc& d) {
         return at;
     };
     L.gen = f64 || generic_hw(d.H, d.W);
+    if (L.gen && !f64) {
+        L.mm = mm_plan((int)H, (int)W);
+        L.mmr = mm_plan_row((int)W);
+    }
     L.spec[0] = take(L.gen ? P * H * (N + 1) * csz : img);
     L.spec[1] = take(img);
     L.rimg = L.gen ? take(img) : 0;
@@ -168,7 +175,7 @@ Layout make_layout(const admm_tv_desc& d) {
     // one Wiener factor per module (its rho); on the fused path followed by their packed copies for
     // the column pass (k_fc_pack)
     // (generic path: a [H][Wh] copy for the matrix-core column pass, k_fc_transpose)
-    L.fcT = take(G * (N + 1) * H * rs * ((!L.gen || (!f64 && mm_plan((int)H, (int)W).ok)) ? 2 : 1));
+    L.fcT = take(G * (N + 1) * H * rs * ((!L.gen || L.mm.ok) ? 2 : 1));
     L.mT = take((N + 1) * H * csz);
     // twiddles; on the generic path followed by the plan's Bluestein tables (make_plan)
     L.twW = take((W + (L.gen ? make_plan((int)W, f64).ntab : 0)) * csz);
@@ -532,7 +539,7 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const T* kern, cons
                                    fc + (size_t)ngroups_of(d) * n, H, N, col_e(H));
                 if (int e = launch_check("k_fc_pack")) return e;
             }
-            if constexpr (std::is_same<T, float>::value) if (Lo.gen && mm_plan(H, W).ok) {
+            if constexpr (std::is_same<T, float>::value) if (Lo.gen && Lo.mm.ok) {
                 float* fc = at<float>(ws, Lo.fcT);  // the generic path has one module
                 hipLaunchKernelGGL(k_fc_transpose, dim3(std::min(4096, (n + nt - 1) / nt)), dim3(nt), 0, s, fc, fc + n, H,
                                    N + 1);
@@ -1100,11 +1107,12 @@ template <int S> int grow_inv_mm_launch(const GRowInvMMArgs& a, size_t lds, int 
     hipLaunchKernelGGL(k_grow_inv_mm<S>, grid, dim3(256), lds, s, a);
     return launch_check("k_grow_inv_mm");
 }
+// mmr: the layout's row-inverse plan (Layout::mmr)
 template <class T>
 int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long rows, hipStream_t s,
-             cx_t<T>* gscr = nullptr) {
+             cx_t<T>* gscr, const MMPlan& mmr) {
     if constexpr (!kF64<T>) {
-        const MMPlan m = mm_plan_row(W);
+        const MMPlan m = mmr;
         if (m.ok && rows > 0) {
             const int Wh = W / 2 + 1;
             GRowInvMMArgs a{spec, img, tw, rows, W, m.R, m.h, m.KS, m.MT, m.NL, m.RP, Wh, 2 * m.NL * Wh * 2};
@@ -1177,11 +1185,12 @@ template <int S> int gcol_mm_launch(const GColMMArgs& a, size_t lds, hipStream_t
 #endif
 inline int mm_dbg() { return ADMM_MM_DBG_BUILD ? env_int("ADMM_MM_DBG", 0) : 0; }
 
+// mm: the layout's column-pass plan (Layout::mm; its factor copy was sized and written for it)
 template <class T>
 int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx_t<T>* tw, int H, int W, long long P,
-         int mode, hipStream_t s, cx_t<T>* gscr = nullptr) {
+         int mode, hipStream_t s, cx_t<T>* gscr, const MMPlan& mm) {
     if constexpr (!kF64<T>) {
-        const MMPlan m = mm_plan(H, W);
+        const MMPlan m = mm;
         if (mode == 0 && m.ok) {  // the factor's [H][Wh] copy follows fcT (setup, k_fc_transpose)
             const int Wh = W / 2 + 1;
             GColMMArgs a{spec, dump, fcT + (size_t)Wh * H, tw, H, m.R, m.h, m.KS, m.MT, m.NL, __builtin_ctz(m.NL), m.RP,
@@ -1225,9 +1234,10 @@ int gapply(const T* img_in, T* img_out, cx_t<T>* spec, const Layout& Lo, void* w
     C* twW = at<C>(ws, Lo.twW);
     C* gs = at<C>(ws, Lo.gscr);
     if (int e = grow_fwd(img_in, spec, twW, W, rows, s, gs)) return e;
-    if (int e = gcol<T>(spec, nullptr, at<T>(ws, Lo.fcT), at<C>(ws, Lo.mT), at<C>(ws, Lo.twH), H, W, P, mode, s, gs))
+    if (int e = gcol<T>(spec, nullptr, at<T>(ws, Lo.fcT), at<C>(ws, Lo.mT), at<C>(ws, Lo.twH), H, W, P, mode, s, gs,
+                        Lo.mm))
         return e;
-    return grow_inv<T>(spec, img_out, twW, W, rows, s, gs);
+    return grow_inv<T>(spec, img_out, twW, W, rows, s, gs, Lo.mmr);
 }
 
 template <class T> int gstep(const GStepArgsT<T>& a, bool iso, bool first, bool hist, hipStream_t s) {
@@ -1346,8 +1356,8 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
         const bool last = it == d.maxit;
         {
             ProfScope ps(1, st);
-            if (int e = gcol<T>(cspec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, np, 0, st, gs)) return e;
-            if (int e = grow_inv<T>(cspec, last ? cout : cx, twW, W, crows, st, gs)) return e;
+            if (int e = gcol<T>(cspec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, np, 0, st, gs, Lo.mm)) return e;
+            if (int e = grow_inv<T>(cspec, last ? cout : cx, twW, W, crows, st, gs, Lo.mmr)) return e;
         }
         if (last && !train) break;
         const T* xk = last ? cout : cx;
@@ -1632,9 +1642,10 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
         B.R = strip_rows((int)d.H, (int)d.W / 2, rows);
         B.nstrips = rows / B.R;
     }
-    B.part = take((size_t)std::max(d.maxit, 1) * B.nstrips * 2 * rs);
+    // the lambda / rho gradient partials are fp64 in every solve (admm_backward.hpp)
+    B.part = take((size_t)std::max(d.maxit, 1) * B.nstrips * 2 * sizeof(double));
     B.ntp = 256;
-    B.tpart = take((size_t)std::max(d.maxit, 1) * G * B.ntp * rs);  // [K][G][ntp]
+    B.tpart = take((size_t)std::max(d.maxit, 1) * G * B.ntp * sizeof(double));  // [K][G][ntp]
     B.q = take(G * 2 * (size_t)d.H * d.W * rs);
     if (d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) {
         const size_t nf = ((size_t)d.W / 2 + 1) * d.H;
@@ -1687,10 +1698,10 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, c
     T* ab[4] = {at<T>(ws, BL.abar[0]), at<T>(ws, BL.abar[1]), at<T>(ws, BL.abar[2]),
                     at<T>(ws, BL.abar[3])};
     T* bbar = (d.kh == 0 && gxin) ? gxin : at<T>(ws, BL.bbar);
-    T* part = at<T>(ws, BL.part);
-    T* tpart = at<T>(ws, BL.tpart);
+    double* part = at<double>(ws, BL.part);
+    double* tpart = at<double>(ws, BL.tpart);
     T* q = at<T>(ws, BL.q);
-    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * BL.ntp * sizeof(T), s));
+    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * BL.ntp * sizeof(double), s));
     const T* xbk = gout;
     int ain = 0, xo = 0;
     for (int k = K; k >= 1; --k) {
@@ -1700,8 +1711,8 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, c
             // r^_k = M x^_k; with the PSF gradient the column pass also dumps X^_k's spectrum and
             // A += fc^2 Re(sum_p conj(X^_k) R_k)
             if (int e = grow_fwd(xbk, spec, twW, W, rows, s, gs)) return e;
-            if (int e = gcol<T>(spec, xspec, fcT, at<C>(ws, Lo.mT), twH, H, W, P, 0, s, gs)) return e;
-            if (int e = grow_inv<T>(spec, rb, twW, W, rows, s, gs)) return e;
+            if (int e = gcol<T>(spec, xspec, fcT, at<C>(ws, Lo.mT), twH, H, W, P, 0, s, gs, Lo.mm)) return e;
+            if (int e = grow_inv<T>(spec, rb, twW, W, rows, s, gs, Lo.mmr)) return e;
             if (psf_grad) {
                 hipLaunchKernelGGL(k_gxspec_acc<T>, fgrid, fblk, 0, s, xspec, ht(k), P, H, Wh, fcT, at<double2>(ws, BL.aacc));
                 if (int e = launch_check("k_gxspec_acc")) return e;
@@ -1745,9 +1756,9 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, c
     }
     if (psf_grad) {  // Z = sum_p conj(Bbar_p) Xin_p, then the k x k taps
         if (int e = grow_fwd(bbar, spec, twW, W, rows, s, gs)) return e;
-        if (int e = gcol<T>(spec, xspec, nullptr, nullptr, twH, H, W, P, 3, s, gs)) return e;
+        if (int e = gcol<T>(spec, xspec, nullptr, nullptr, twH, H, W, P, 3, s, gs, Lo.mm)) return e;
         if (int e = grow_fwd(xin, spec, twW, W, rows, s, gs)) return e;
-        if (int e = gcol<T>(spec, spec, nullptr, nullptr, twH, H, W, P, 3, s, gs)) return e;
+        if (int e = gcol<T>(spec, spec, nullptr, nullptr, twH, H, W, P, 3, s, gs, Lo.mm)) return e;
         hipLaunchKernelGGL(k_gxspec_acc<T>, fgrid, fblk, 0, s, xspec, spec, P, H, Wh, nullptr, at<double2>(ws, BL.zacc));
         if (int e = launch_check("k_gxspec_acc")) return e;
         hipLaunchKernelGGL(k_psf_grad<T>, dim3(d.kh * d.kw), dim3(256), 0, s, at<double2>(ws, BL.aacc),
@@ -1936,11 +1947,11 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
                     at<float>(ws, BL.abar[3])};
     // b^ accumulates straight into gxin when there is no PSF and one module (x^_in = b^)
     float* bbar = (d.kh == 0 && gxin && G == 1) ? gxin : at<float>(ws, BL.bbar);
-    float* part = at<float>(ws, BL.part);
-    float* tpart = at<float>(ws, BL.tpart);
+    double* part = at<double>(ws, BL.part);
+    double* tpart = at<double>(ws, BL.tpart);
     float* q = at<float>(ws, BL.q);
     const long long rows = P * H;
-    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * G * BL.ntp * sizeof(float), s));
+    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * G * BL.ntp * sizeof(double), s));
     int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(gout, spec[0], twW, rows, s); });
     if (e) return e;
     int cur = 0, ain = 0;

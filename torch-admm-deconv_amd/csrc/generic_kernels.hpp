@@ -862,7 +862,7 @@ template <class T> struct GBwdArgsT {
     const T* qp;          // iso: Q_{k-1}  [2][H][W]
     const T* lam;
     const T* rho;
-    T* part;              // per block {rho^, tau^}
+    double* part;         // per block {rho^, tau^}, fp64
     int H, W;
     long long npx;
 };
@@ -877,9 +877,9 @@ __device__ __forceinline__ T gabar(T d, T ap, T ub, T tau, T rho, T n, T q) {
 
 template <bool ISO, bool LASTK, bool FIRSTK, class T = float>
 __global__ void __launch_bounds__(256) k_gbwd(GBwdArgsT<T> a) {
-    __shared__ T red[2][256];
+    __shared__ double red[2][256];  // the lambda / rho partials reduce in fp64
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    T rho_acc = 0, tau_acc = 0;
+    double rho_acc = 0.0, tau_acc = 0.0;
     if (idx < a.npx) {
         const int H = a.H, W = a.W;
         const long long HW = (long long)H * W;
@@ -910,7 +910,7 @@ __global__ void __launch_bounds__(256) k_gbwd(GBwdArgsT<T> a) {
         {
             const T ex = (T(2) * zpx - apx0) - (a.akx[P0] - apx0 + zpx);
             const T ey = (T(2) * zpy - apy0) - (a.aky[P0] - apy0 + zpy);
-            rho_acc = fmat(dx0, ex, dy0 * ey);
+            rho_acc = fma((double)dx0, (double)ex, (double)dy0 * (double)ey);
         }
         // b^ += r^
         a.bbar[P0] = LASTK ? r0 : a.bbar[P0] + r0;
@@ -936,7 +936,7 @@ __global__ void __launch_bounds__(256) k_gbwd(GBwdArgsT<T> a) {
             a.xb[P0] = (abx0 - abxR) + (aby0 - abyD);
             if constexpr (!ISO) {
                 const T wbx = rho * dx0, wby = rho * dy0;
-                tau_acc = soft_dtau(apx0, T(2) * wbx - ubx0, tau) + soft_dtau(apy0, T(2) * wby - uby0, tau);
+                tau_acc = (double)soft_dtau(apx0, T(2) * wbx - ubx0, tau) + (double)soft_dtau(apy0, T(2) * wby - uby0, tau);
             }
         }
     }
