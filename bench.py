@@ -170,7 +170,7 @@ def generic_extras(dev, no_parity, keys=("bsd", "hd")):
         npx = B * C * H * W
         e = {"value": maxit / dt, "unit": "iterations/s", "ms_per_step": dt * 1e3, "steps": steps,
              "us_per_iter_per_Mpx": dt / maxit / (npx / 1e6) * 1e6, "workload": desc,
-             "path": "fused" if _native.load().admm_tv_supported(H, W) == 1 else "generic"}
+             "path": {1: "fused", 3: "fused mixed-radix"}.get(_native.load().admm_tv_supported(H, W), "generic")}
         if not no_parity:
             from oracle.admm_oracle import rel_l2, solve_fourier
             ref = solve_fourier(x[:1, :1].double().cpu(), 0.01, 0.02, psf.double().cpu(), iso, maxit)
@@ -191,7 +191,7 @@ def generic_extras(dev, no_parity, keys=("bsd", "hd")):
                 del os.environ["ADMM_GEN_STREAMS"]
             else:
                 os.environ["ADMM_GEN_STREAMS"] = old
-        generic = e["path"] == "generic"
+        generic = e["path"] == "generic"  # the fused paths (power-of-two and mixed-radix) keep pass A / B bytes
         ba = (2 * PASS_A_FIRST_BYTES + (cnt[0] - 2) * PASS_A_BYTES) * npx
         bb = cnt[1] * (GEN_COL_BYTES if generic else PASS_B_BYTES) * npx
         per = {}

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ADMM_TV_ABI_VERSION 5
+#define ADMM_TV_ABI_VERSION 6
 
 enum {
     ADMM_TV_OK = 0,
@@ -100,6 +100,11 @@ int admm_tv_abi_version(void);
 const char* admm_tv_build_hash(void);
 
 /* 1: (H, W) runs on the fused power-of-two kernels (H in [16,4096], W in [16,2048]);
+ * 3: a smooth size (2^a 3^b 5^c with a transform plan: W/2 in {240, 320, 360, 480, 540, 640, 960} or a
+ *    power of two up to 1024, H in {240, 360, 480, 540, 720, 960, 1080, 2160} or a power of two up to
+ *    4096, e.g. 1080x1920, 720x1280, 480x640): admm_tv_forward runs the same fused two-pass iteration
+ *    with mixed-radix register transforms (ABI v6); the training forward / backward of these sizes
+ *    run on the generic kernels, as for 2;
  * 2: any other size up to 65,536 points per side, run on the generic kernels (mixed-radix
  *    transforms, per-pixel step; the reference accepts any size, deconv.py:103-106): lines up to
  *    10,240 points transform in the kernels' LDS image, longer ones in a global scratch slot per

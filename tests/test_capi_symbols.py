@@ -49,12 +49,15 @@ def test_library_is_gfx950_code():
 def test_host_entry_points():
     from admmtor import _native
     lib = _native.load()
-    assert lib.admm_tv_abi_version() == 5
+    assert lib.admm_tv_abi_version() == 6
     fast, generic = 1, 2
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
     assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 4096), (8, 64), (1, 1), (481, 321))] == [generic] * 5
     assert [lib.admm_tv_supported(*hw) for hw in ((4097, 16), (5000, 33))] == [generic] * 2  # beyond 4096
     assert [lib.admm_tv_supported(*hw) for hw in ((65537, 16), (16, 70000), (0, 16))] == [0] * 3
+    # smooth sizes with transform plans: the fused iteration on mixed-radix transforms (inference)
+    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1920), (720, 1280), (480, 640), (2160, 512))] == [3] * 4
+    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 3840), (1081, 1920), (1080, 1918))] == [generic] * 3
     d = _native.desc(64, 3, 1024, 1024, 21, False, 50)
     ws = _native.workspace_size(d)
     img = 64 * 3 * 1024 * 1024 * 4

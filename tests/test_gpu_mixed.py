@@ -1,0 +1,107 @@
+"""The fused two-pass iteration at smooth sizes (mixed-radix register transforms, mixed_kernels.hpp;
+admm_tv_supported == 3): HD, 720p, VGA and other 2^a 3^b 5^c frames, and power-of-two widths / heights
+paired with a smooth other side.  The reference runs every H, W through the same op sequence
+(deconv.py:42,104-106); here each case is checked against the fp64 oracle (north-star gate 1e-5) and
+against the generic kernels' solve of the same input (ADMM_MIXED=0: the same algorithm with other
+roundings, so the two agree to fp32 noise)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TOL_REF64 = 1e-5
+
+
+def rel(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return ((a - b).norm() / b.norm()).item()
+
+
+def solve(x, k, iso, it, dev, lam=0.01, rho=0.02):
+    from admmtor.eops.deconv import fft_admm_tv
+    kk = k.to(dev) if k is not None else torch.empty(0, device=dev)
+    out = fft_admm_tv(x.to(dev), lam, rho, kk, iso, it)
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+def oracle(x, k, iso, it, lam=0.01, rho=0.02):
+    from oracle.admm_oracle import solve_fourier
+    kk = k.double() if k is not None else torch.empty(0, dtype=torch.float64)
+    return solve_fourier(x.double(), lam, rho, kk, iso, it)
+
+
+def test_supported_codes():
+    from admmtor import _native
+    lib = _native.load()
+    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1920), (720, 1280), (480, 640), (2160, 1024), (1024, 960),
+                                                  (540, 1080), (360, 720), (240, 480))] == [3] * 8
+    assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (4096, 2048))] == [1] * 2
+    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1921), (1080, 3840), (1000, 1920), (481, 321))] == [2] * 4
+
+
+CASES = [
+    # (B, C, H, W), psf, iso, iterations
+    ((1, 3, 1080, 1920), ("gauss:1.5", 9), False, 20),   # HD frame: rows 960 = 16*4*15, columns 1080 = 9*15*8
+    ((2, 3, 720, 1280), ("motion", 15), False, 15),      # 720p: rows 640 = 16*4*10, columns 720 = 9*16*5
+    ((2, 2, 480, 640), ("gauss:1.5", 7), True, 20),      # VGA, iso: rows 320 = 16*2*10 (32-lane groups)
+    ((3, 1, 240, 480), None, True, 12),                  # 16-lane row groups, no PSF
+    ((1, 2, 360, 720), ("motion", 9), False, 10),        # 24 active pixel lanes of 32
+    ((1, 1, 540, 1080), ("gauss:2", 9), True, 10),       # 36 active pixel lanes, 9-point spectrum edge
+    ((1, 1, 2160, 1024), ("gauss:2", 11), False, 6),     # power-of-two rows, 2160-point columns (9*16*15)
+    ((2, 1, 1024, 960), ("gauss:1.5", 9), False, 8),     # power-of-two columns, 480-point rows
+    ((1, 2, 960, 512), None, True, 8),                   # 960-point columns (15*16*4)
+    ((1, 1, 1080, 1920), ("random", 5), True, 3),        # iso, non-centrosymmetric PSF, 3 iterations
+    ((2, 1, 720, 1280), None, False, 1),                 # one iteration
+]
+
+
+@pytest.mark.parametrize("shape,psf,iso,it", CASES)
+def test_mixed_vs_oracle_and_generic(cuda_dev, monkeypatch, shape, psf, iso, it):
+    from admmtor import _native
+    from admmtor.synth import blurred_batch, make_psf
+    assert _native.load().admm_tv_supported(shape[2], shape[3]) == 3
+    k = make_psf(*psf) if psf else None
+    x = blurred_batch(*shape, k if k is not None else torch.empty(0), seed=sum(shape) + it)
+    got = solve(x, k, iso, it, cuda_dev)
+    ref = oracle(x, k, iso, it)
+    monkeypatch.setenv("ADMM_MIXED", "0")  # the same solve on the generic kernels
+    gen = solve(x, k, iso, it, cuda_dev)
+    e_ref, e_gen, e_gen_ref = rel(got, ref), rel(got, gen), rel(gen, ref)
+    print(shape, psf, "iso" if iso else "aniso", it, f"mixed vs fp64 oracle {e_ref:.2e}, vs generic {e_gen:.2e} "
+          f"(generic vs oracle {e_gen_ref:.2e})")
+    assert e_ref <= TOL_REF64
+    assert e_gen <= 2 * max(e_gen_ref, 1e-7) + e_ref
+
+
+def test_mixed_planes_independent(cuda_dev):
+    """aniso planes are independent: a plane solved inside a batch equals the plane solved alone, bit
+    for bit (no cross-plane state in the strips / column blocks)."""
+    from admmtor.synth import blurred_batch, make_psf
+    k = make_psf("gauss:1.5", 9)
+    x = blurred_batch(3, 2, 720, 1280, k, seed=5)
+    full = solve(x, k, False, 10, cuda_dev)
+    one = solve(x[1:2, 1:2].contiguous(), k, False, 10, cuda_dev)
+    assert torch.equal(full[1:2, 1:2], one)
+
+
+def test_mixed_autograd_uses_generic_training(cuda_dev):
+    """Training at a smooth size: the forward with history and the backward run on the generic kernels
+    (the inference solve on the fused mixed kernels); the output of the training forward equals the
+    generic inference solve and its gradients match the oracle's autograd."""
+    from admmtor.eops.deconv import fft_admm_tv
+    from admmtor.synth import blurred_batch
+    from oracle.admm_oracle import solve_fourier
+    x = blurred_batch(1, 2, 240, 480, torch.empty(0), seed=8)
+    cot = torch.randn(x.shape, generator=torch.Generator().manual_seed(1))
+    xg = x.to(cuda_dev).requires_grad_(True)
+    lam = torch.tensor([0.03], device=cuda_dev, requires_grad=True)
+    out = fft_admm_tv(xg, lam, 0.05, torch.empty(0, device=cuda_dev), True, 8)
+    gx, gl = torch.autograd.grad(out, (xg, lam), cot.to(cuda_dev))
+    xr = x.double().requires_grad_(True)
+    lr = torch.tensor([0.03], dtype=torch.float64, requires_grad=True)
+    ref = solve_fourier(xr, lr, 0.05, torch.empty(0, dtype=torch.float64), True, 8)
+    rgx, rgl = torch.autograd.grad(ref, (xr, lr), cot.double())
+    e = (rel(out.detach().cpu(), ref.detach()), rel(gx.cpu(), rgx), rel(gl.cpu(), rgl))
+    print("240x480 training:", e)
+    assert e[0] <= TOL_REF64 and e[1] <= 1e-4 and e[2] <= 1e-4

@@ -102,24 +102,29 @@ def _direct_iso(xl, k, lam, rho, maxit):
 
 
 def _rho_grad_noise(B):
-    """How far the reference formulation's fp32 rho gradient sits from its fp64 one on this test's
-    input (fp32 vs fp64 autograd through the oracle's restatement, CPU).  The rho gradient of this
-    iso solve is ill-conditioned: a 1e-7 relative perturbation of the per-pixel norm sums alone moves
-    it by ~1.4e-4, so the fp32 reassociation of those sums across ranks cannot be held
-    to a fixed 1e-4; the gate is this measured noise floor instead (the fp64 runs below show the
-    sharding itself is exact to ~1e-12)."""
+    """How far the reference formulation's own fp32 rho gradient moves under the reassociation that
+    sharding performs: the oracle's restatement (CPU) in fp32 with the batch in four orders -- the
+    per-pixel norm (deconv.py:23-24) then sums the same (B, C) terms in another order -- each against
+    its fp64 gradient; the largest distance.  This rho gradient is a sum of large cancelling terms: one
+    fp32 evaluation of it lands anywhere from ~5e-7 to ~3e-4 from fp64 depending on the rounding
+    pattern (measured; fp64 arithmetic with the norm sums perturbed by one fp32 ulp moves it only
+    1e-7..1e-6, DESIGN.md §6), so the sharded fp32 solve is gated by this spread, not a fixed 1e-4;
+    the fp64 runs below show the sharding itself is exact to ~1e-13."""
     from admmtor.synth import blurred_batch, make_psf
     from oracle.admm_oracle import solve_fourier
     k = make_psf("motion", 7)
     full = blurred_batch(B, 3, 64, 128, k, seed=21)
     cot = torch.randn(full.shape, generator=torch.Generator().manual_seed(5))
-    g = []
-    for dt in (torch.float32, torch.float64):
+
+    def grad(dt, order):
         lam = torch.tensor([0.02], dtype=dt, requires_grad=True)
         rho = torch.tensor([0.05], dtype=dt, requires_grad=True)
-        out = solve_fourier(full.to(dt), lam, rho, k.to(dt), True, 15)
-        g.append(torch.autograd.grad((out * cot.to(dt)).sum(), rho)[0].double().item())
-    return abs(g[0] - g[1]) / abs(g[1])
+        out = solve_fourier(full[order].to(dt), lam, rho, k.to(dt), True, 15)
+        return torch.autograd.grad((out * cot[order].to(dt)).sum(), rho)[0].double().item()
+    ident = torch.arange(B)
+    g64 = grad(torch.float64, ident)
+    orders = [ident, ident.flip(0), ident.roll(B // 2), torch.randperm(B, generator=torch.Generator().manual_seed(0))]
+    return max(abs(grad(torch.float32, o) - g64) / abs(g64) for o in orders)
 
 
 @pytest.mark.parametrize("world,iso,B,f64", [(2, False, 5, False), (2, True, 5, False), (2, True, 1, False),

@@ -79,7 +79,7 @@ class AdmmTvDesc(ctypes.Structure):
 
 ADMM_TV_FLAG_PSF_GRAD = 1
 ADMM_TV_FLAG_F64 = 2  # fp64 solve: the *_f64 entry points, double arrays
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class NativeError(RuntimeError):

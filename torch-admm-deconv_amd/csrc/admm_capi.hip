@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "gcol_mm.hpp"
+#include "mixed_capi.hpp"
 #include "admm_tv.h"
 
 using namespace admm;
@@ -104,6 +105,16 @@ bool generic_hw(int64_t H, int64_t W) {
     return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax && gen_fits((int)H) &&
            gen_fits((int)W);
 }
+int env_int(const char* name, int dflt);
+// smooth sizes on the fused two-pass iteration with mixed-radix register transforms (mixed_kernels.hpp,
+// DESIGN.md §7c): W even with a row plan for W / 2, a column plan for H, not both powers of two (those
+// are supported_hw).  Inference only: the training forward / backward of these sizes stay generic.
+// ADMM_MIXED=0 (A/B knob) keeps them on the generic kernels.
+bool mixed_hw(int64_t H, int64_t W) {
+    if (supported_hw(H, W) || H < 16 || W < 16 || (W & 1) || H > 4096 || W > 2048) return false;
+    if (!admm_mixed::row_ok((int)(W / 2)) || !admm_mixed::col_ok((int)H)) return false;
+    return (W / 2) % admm_mixed::col_cols((int)H) == 0 && env_int("ADMM_MIXED", 1) != 0;
+}
 // fp64 solves (ADMM_TV_FLAG_F64) run on the generic kernels' double instantiation at every size
 bool is_f64(const admm_tv_desc& d) { return (d.flags & ADMM_TV_FLAG_F64) != 0; }
 bool f64_hw(int64_t H, int64_t W) {
@@ -139,6 +150,9 @@ struct Layout {
     // generic path: the matrix-core plans, decided once per call (their environment knobs are read
     // here only, so the regions sized below and the kernels launched later always agree)
     MMPlan mm, mmr;
+    // mixed-radix fused inference (mixed_hw; run_forward_mixed): the Wiener factor for its column pass
+    bool mixed;
+    size_t fcM;
     size_t rimg;  // generic path: spec[0] = half spectra [P][H][W/2+1], spec[1] = x image, rimg = r image
     size_t gscr;  // generic path, lines beyond the LDS image: the transform blocks' scratch slots
     int ngroups, ppg;
@@ -165,6 +179,7 @@ Layout make_layout(const admm_tv_desc& d) {
         L.mm = mm_plan((int)H, (int)W);
         L.mmr = mm_plan_row((int)W);
     }
+    L.mixed = L.gen && !f64 && G == 1 && mixed_hw(d.H, d.W);
     L.spec[0] = take(L.gen ? P * H * (N + 1) * csz : img);
     L.spec[1] = take(img);
     L.rimg = L.gen ? take(img) : 0;
@@ -183,6 +198,7 @@ Layout make_layout(const admm_tv_desc& d) {
     L.twHd = take(H * sizeof(double2));
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
     L.gscr = L.gen ? take(glb_scratch((int)H, (int)W, (long long)P, f64)) : 0;
+    L.fcM = L.mixed ? take((N + 1) * H * sizeof(float)) : 0;  // [H][N + 1], k_fc_mixed
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
         // plane groups for the iso norm pass: enough (group,row) items to fill the chip
@@ -538,6 +554,10 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const T* kern, cons
                 hipLaunchKernelGGL(k_fc_pack, dim3((n + nt - 1) / nt), dim3(nt), 0, s, fc,
                                    fc + (size_t)ngroups_of(d) * n, H, N, col_e(H));
                 if (int e = launch_check("k_fc_pack")) return e;
+            }
+            if constexpr (std::is_same<T, float>::value) if (Lo.mixed) {
+                hipError_t e = admm_mixed::fc_mixed(at<float>(ws, Lo.fcT), at<float>(ws, Lo.fcM), H, N, s);
+                if (e != hipSuccess) return fail(ADMM_TV_EHIP, std::string("k_fc_mixed: ") + hipGetErrorString(e));
             }
             if constexpr (std::is_same<T, float>::value) if (Lo.gen && Lo.mm.ok) {
                 float* fc = at<float>(ws, Lo.fcT);  // the generic path has one module
@@ -1442,6 +1462,89 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     return solve_planes(0, P, s);
 }
 
+// rows per strip of the mixed row pass: a divisor of H (8, 4, 2 or 1), halved while there are fewer than
+// ~2 waves per SIMD of strips (the row group of a plan is Lg lanes; rows of 960 and 640 pairs take a
+// whole wave)
+int strip_rows_mixed(int H, long long rows, int lanes) {
+    int R = 8;
+    while (R > 1 && H % R) R /= 2;
+    const long long want = 2LL * 1024 * 64 / std::max(lanes, 1);
+    while (R > 2 && rows / R < want && H % (R / 2) == 0) R /= 2;
+    return R;
+}
+
+// The inference solve of a smooth size (mixed_hw) on the fused two-pass iteration (mixed_kernels.hpp):
+// the same sequence as run_forward's fused loop -- b = H_t(xin) once (here through the generic
+// transforms, mode 1: once per solve), r_1 = rowFFT(b), then per iteration pass B (column FFT, Wiener
+// factor, column IFFT), [iso: the norm pass, its reduce and the cross-rank hook], pass A -- inside
+// the generic layout's regions (spec[0] / spec[1] hold the packed row spectra ping-pong, u[0..3] the
+// u images; the generic b region or xin is b, in pixel order).
+int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin, const float* lam, const float* rho,
+                      float* out, void* ws, hipStream_t s) {
+    const long long P = d.B * d.C;
+    const int H = (int)d.H, W = (int)d.W, N = W / 2;
+    cf* twW = at<cf>(ws, Lo.twW);
+    cf* twH = at<cf>(ws, Lo.twH);
+    const float* fcM = at<float>(ws, Lo.fcM);
+    cf* spec[2] = {at<cf>(ws, Lo.spec[0]), at<cf>(ws, Lo.spec[1])};
+    float* u[4] = {at<float>(ws, Lo.u[0]), at<float>(ws, Lo.u[1]), at<float>(ws, Lo.u[2]), at<float>(ws, Lo.u[3])};
+    auto hchk = [&](hipError_t e, const char* what) {
+        return e == hipSuccess ? 0 : fail(ADMM_TV_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    const long long rows = P * H;
+    const float* bimg = xin;
+    {
+        ProfScope ps(3, s);
+        if (d.kh > 0) {  // b = H_t(xin) once, into the generic b region (half spectra as scratch)
+            float* bb = at<float>(ws, Lo.b);
+            if (int e = gapply<float>(xin, bb, spec[0], Lo, ws, d, 1, s)) return e;
+            bimg = bb;
+        }
+        if (int e = hchk(admm_mixed::r2c(N, bimg, spec[0], twW, rows, s), "k_row_r2c_m")) return e;  // r_1 = b
+    }
+    const int lanes = N >= 640 ? 64 : N >= 320 ? 32 : 16;
+    const int R = strip_rows_mixed(H, rows, lanes);
+    int cur = 0, uin = 0;
+    for (int it = 1; it <= d.maxit; ++it) {
+        {
+            ProfScope ps(1, s);
+            if (int e = hchk(admm_mixed::pass_b(H, spec[cur], fcM, twH, N, P, s), "k_pass_b_m")) return e;
+        }
+        if (it == d.maxit) {
+            ProfScope ps(3, s);
+            return hchk(admm_mixed::c2r(N, spec[cur], out, twW, rows, s), "k_row_c2r_m");
+        }
+        const bool first = it == 1;
+        const float* uxi = u[2 * uin];
+        const float* uyi = u[2 * uin + 1];
+        float* uxo = u[2 * (1 - uin)];
+        float* uyo = u[2 * (1 - uin) + 1];
+        const float* nsq = nullptr;
+        if (d.iso) {
+            ProfScope ps(2, s);
+            float* nout = at<float>(ws, Lo.nsq);
+            IsoArgs ia{spec[cur], uxi, uyi, nullptr, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
+                       (long long)Lo.ngroups * H, P};
+            if (int e = hchk(admm_mixed::iso_norm(N, ia, first, s), "k_iso_norm_m")) return e;
+            const long long n4 = 2LL * H * W / 4;
+            hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, at<float4>(ws, Lo.part),
+                               reinterpret_cast<float4*>(nout), Lo.ngroups, n4);
+            if (int e = launch_check("k_iso_reduce")) return e;
+            allreduce(d, nout, 2ull * H * W, s);  // sharded batch: sums over every rank's planes
+            nsq = nout;
+        }
+        {
+            ProfScope ps(0, s);
+            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, nullptr, lam, rho, twW, H, R,
+                         rows / R, P, 0};
+            if (int e = hchk(admm_mixed::pass_a(N, pa, d.iso != 0, first, s), "k_pass_a_m")) return e;
+        }
+        cur = 1 - cur;
+        uin = 1 - uin;
+    }
+    return 0;
+}
+
 // The forward solver.  hist == nullptr: inference (u ping-pong).  Otherwise training mode:
 // a_k -> hist slot k-1 (x image at 2(k-1), y image at 2(k-1)+1), N_k -> norm slot k-1, and
 // the last iteration's pass A also runs (a_K is needed by the backward).
@@ -1468,6 +1571,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         return 0;
     }
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
+    if (Lo.mixed && !hist) return run_forward_mixed(d, Lo, xin, lam, rho, out, ws, s);
     if (Lo.gen) return run_forward_gen(d, Lo, xin, lam, rho, out, ws, hist, s);
     cf* twW = at<cf>(ws, Lo.twW);
     cf* twH = at<cf>(ws, Lo.twH);
@@ -1830,7 +1934,9 @@ extern "C" {
 
 int admm_tv_abi_version(void) { return ADMM_TV_ABI_VERSION; }
 
-int admm_tv_supported(int64_t H, int64_t W) { return supported_hw(H, W) ? 1 : generic_hw(H, W) ? 2 : 0; }
+int admm_tv_supported(int64_t H, int64_t W) {
+    return supported_hw(H, W) ? 1 : mixed_hw(H, W) ? 3 : generic_hw(H, W) ? 2 : 0;
+}
 
 int admm_tv_supported_f64(int64_t H, int64_t W) { return f64_hw(H, W) ? 1 : 0; }
 

@@ -320,7 +320,7 @@ template <int H, int C> struct ColGeom {
 
 // Packed copy of one module's Wiener factors for the column pass: fcP[(kx L + t) E + j] =
 // fcT[kx H + t + L j] (the E factors a column-pass thread multiplies, contiguous)
-__global__ void k_fc_pack(const float* __restrict__ fcT, float* __restrict__ fcP, int H, int N, int E) {
+static __global__ void k_fc_pack(const float* __restrict__ fcT, float* __restrict__ fcP, int H, int N, int E) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (N + 1) * H) return;
     const int L = H / E, kx = i / H, r = i % H, t = r / E, j = r % E;
@@ -913,7 +913,7 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
 }
 
 // nsq[k] = sum_g partial[g][k], k over 2*H*W, fixed order (deterministic)
-__global__ void k_iso_reduce(const float4* __restrict__ partial, float4* __restrict__ nsq, int ngroups,
+static __global__ void k_iso_reduce(const float4* __restrict__ partial, float4* __restrict__ nsq, int ngroups,
                              long long n4) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;

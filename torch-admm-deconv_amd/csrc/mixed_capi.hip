@@ -1,0 +1,155 @@
+// mixed_capi.hip -- launchers of the mixed-radix fused kernels (mixed_kernels.hpp):
+// the plan tables dispatched to their template instances.  The solve itself is orchestrated in
+// admm_capi.hip (run_forward_mixed).
+#include <type_traits>
+
+#include "mixed_capi.hpp"
+#include "mixed_kernels.hpp"
+
+using namespace admm;
+
+namespace admm_mixed {
+
+namespace {
+
+template <class F> hipError_t with_row(int N, F&& f) {
+    switch (N) {
+        case 16: return f(std::integral_constant<int, 16>{});
+        case 32: return f(std::integral_constant<int, 32>{});
+        case 64: return f(std::integral_constant<int, 64>{});
+        case 128: return f(std::integral_constant<int, 128>{});
+        case 256: return f(std::integral_constant<int, 256>{});
+        case 512: return f(std::integral_constant<int, 512>{});
+        case 1024: return f(std::integral_constant<int, 1024>{});
+        case 240: return f(std::integral_constant<int, 240>{});
+        case 320: return f(std::integral_constant<int, 320>{});
+        case 360: return f(std::integral_constant<int, 360>{});
+        case 480: return f(std::integral_constant<int, 480>{});
+        case 540: return f(std::integral_constant<int, 540>{});
+        case 640: return f(std::integral_constant<int, 640>{});
+        case 960: return f(std::integral_constant<int, 960>{});
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <class F> hipError_t with_col(int H, F&& f) {
+    switch (H) {
+        case 16: return f(std::integral_constant<int, 16>{});
+        case 32: return f(std::integral_constant<int, 32>{});
+        case 64: return f(std::integral_constant<int, 64>{});
+        case 128: return f(std::integral_constant<int, 128>{});
+        case 256: return f(std::integral_constant<int, 256>{});
+        case 512: return f(std::integral_constant<int, 512>{});
+        case 1024: return f(std::integral_constant<int, 1024>{});
+        case 2048: return f(std::integral_constant<int, 2048>{});
+        case 4096: return f(std::integral_constant<int, 4096>{});
+        case 240: return f(std::integral_constant<int, 240>{});
+        case 360: return f(std::integral_constant<int, 360>{});
+        case 480: return f(std::integral_constant<int, 480>{});
+        case 540: return f(std::integral_constant<int, 540>{});
+        case 720: return f(std::integral_constant<int, 720>{});
+        case 960: return f(std::integral_constant<int, 960>{});
+        case 1080: return f(std::integral_constant<int, 1080>{});
+        case 2160: return f(std::integral_constant<int, 2160>{});
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <class K> hipError_t lds(K kern, size_t bytes) {
+    if (bytes <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes);
+}
+
+template <int N> unsigned row_blocks(long long items) { return (unsigned)((items + MRowG<N>::SG - 1) / MRowG<N>::SG); }
+
+}  // namespace
+
+bool row_ok(int N) {
+    return with_row(N, [](auto) { return hipSuccess; }) == hipSuccess;
+}
+bool col_ok(int H) {
+    return with_col(H, [](auto) { return hipSuccess; }) == hipSuccess;
+}
+int col_cols(int H) {
+    int c = 0;
+    (void)with_col(H, [&](auto h) {
+        c = MColG<decltype(h)::value>::C;
+        return hipSuccess;
+    });
+    return c;
+}
+
+hipError_t r2c(int N, const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s) {
+    return with_row(N, [&](auto n) {
+        constexpr int NN = decltype(n)::value;
+        using G = MRowG<NN>;
+        if (hipError_t e = lds(k_row_r2c_m<NN>, G::lds_bytes())) return e;
+        hipLaunchKernelGGL(k_row_r2c_m<NN>, dim3(row_blocks<NN>(rows)), dim3(G::NT), G::lds_bytes(), s, img, spec, twW, rows);
+        return hipGetLastError();
+    });
+}
+
+hipError_t c2r(int N, const cf* spec, float* img, const cf* twW, long long rows, hipStream_t s) {
+    return with_row(N, [&](auto n) {
+        constexpr int NN = decltype(n)::value;
+        using G = MRowG<NN>;
+        if (hipError_t e = lds(k_row_c2r_m<NN>, G::lds_bytes())) return e;
+        hipLaunchKernelGGL(k_row_c2r_m<NN>, dim3(row_blocks<NN>(rows)), dim3(G::NT), G::lds_bytes(), s, spec, img, twW, rows);
+        return hipGetLastError();
+    });
+}
+
+hipError_t pass_a(int N, const PassAArgs& a, bool iso, bool first, hipStream_t s) {
+    return with_row(N, [&](auto n) {
+        constexpr int NN = decltype(n)::value;
+        using G = MRowG<NN>;
+        const dim3 grid(row_blocks<NN>(a.nstrips)), blk(G::NT);
+        const size_t l = G::lds_bytes();
+        auto go = [&](auto kern) {
+            if (hipError_t e = lds(kern, l)) return e;
+            hipLaunchKernelGGL(kern, grid, blk, l, s, a);
+            return hipGetLastError();
+        };
+        if (iso) return first ? go(k_pass_a_m<NN, true, true>) : go(k_pass_a_m<NN, true, false>);
+        return first ? go(k_pass_a_m<NN, false, true>) : go(k_pass_a_m<NN, false, false>);
+    });
+}
+
+hipError_t iso_norm(int N, const IsoArgs& a, bool first, hipStream_t s) {
+    return with_row(N, [&](auto n) {
+        constexpr int NN = decltype(n)::value;
+        using G = MRowG<NN>;
+        const dim3 grid(row_blocks<NN>(a.nitems)), blk(G::NT);
+        const size_t l = G::lds_bytes();
+        auto go = [&](auto kern) {
+            if (hipError_t e = lds(kern, l)) return e;
+            hipLaunchKernelGGL(kern, grid, blk, l, s, a);
+            return hipGetLastError();
+        };
+        return first ? go(k_iso_norm_m<NN, true>) : go(k_iso_norm_m<NN, false>);
+    });
+}
+
+hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s) {
+    return with_col(H, [&](auto h) {
+        constexpr int HH = decltype(h)::value;
+        using G = MColG<HH>;
+        const int colblocks = N / G::C;
+        // plane groups of two at H >= 1024 (k_pass_b's measured tile order), plane-major below
+        const int order = HH >= 1024 ? 2 : 1;
+        if (hipError_t e = lds(k_pass_b_m<HH>, G::lds_bytes())) return e;
+        hipLaunchKernelGGL(k_pass_b_m<HH>, dim3((unsigned)(P * colblocks)), dim3(G::NT), G::lds_bytes(), s, spec, fcM, twH,
+                           N, colblocks, order);
+        return hipGetLastError();
+    });
+}
+
+hipError_t fc_mixed(const float* fcT, float* fcM, int H, int N, hipStream_t s) {
+    const long long n = (long long)H * (N + 1);
+    hipLaunchKernelGGL(k_fc_mixed, dim3((unsigned)std::min<long long>(4096, (n + 255) / 256)), dim3(256), 0, s, fcT, fcM,
+                       H, N);
+    return hipGetLastError();
+}
+
+}  // namespace admm_mixed

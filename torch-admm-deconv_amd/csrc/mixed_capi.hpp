@@ -1,0 +1,25 @@
+// mixed_capi.hpp -- launchers of the mixed-radix fused kernels (mixed_kernels.hpp), compiled in their
+// own translation unit (mixed_capi.hip) and called by the solver's orchestration in admm_capi.hip.
+// Every launcher returns hipSuccess or the launch error.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "admm_kernels.hpp"
+
+namespace admm_mixed {
+
+using admm::cf;
+
+// plans exist for the row length N = W/2 / the column length H
+bool row_ok(int N);
+bool col_ok(int H);
+int col_cols(int H);  // columns per column-pass block (N must be a multiple)
+
+hipError_t r2c(int N, const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s);
+hipError_t c2r(int N, const cf* spec, float* img, const cf* twW, long long rows, hipStream_t s);
+hipError_t pass_a(int N, const admm::PassAArgs& a, bool iso, bool first, hipStream_t s);
+hipError_t iso_norm(int N, const admm::IsoArgs& a, bool first, hipStream_t s);
+hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s);
+hipError_t fc_mixed(const float* fcT, float* fcM, int H, int N, hipStream_t s);
+
+}  // namespace admm_mixed

@@ -1,0 +1,589 @@
+// mixed_kernels.hpp -- the fused two-pass ADMM iteration (admm_kernels.hpp) at smooth image sizes
+// (H, W with factors 2, 3, 5 only, W even), e.g. 1080 x 1920, 720 x 1280, 480 x 640 (gfx950).
+//
+// Same algorithm, data layout and bytes as the power-of-two path: pass B is the
+// column FFT -> Wiener factor -> column IFFT in place, pass A the row pass that inverts the row
+// spectra of a strip of R rows (+ one halo row), forms Dx, Dy, the shrink, the dual update, D^T w,
+// r = b + rho v and the r row spectra -- 36 B/px per iteration (48 iso), against the generic path's
+// three transform launches per iteration (~44-60 B/px, §7a).  The transforms are mixed_fft.hpp's
+// guarded Stockham schedules; a plan per length fixes the lanes and the edge layouts:
+//   rows (MRow<N>, N = W/2 complex points):  a row group of Lg lanes (power of two <= 64, within one
+//     wave); pixels in layout(Ep) over Lp = N/Ep lanes (Ep pixel pairs per lane: pair t + Lp j), row
+//     spectra in layout(Es) over Ls = N/Es lanes (element t + Ls j); the inverse schedule runs
+//     Es ... Ep, the forward one Ep ... Es.
+//   columns (MCol<H>): Lc threads per column, C columns per block (ColBuf interleave); column values in
+//     layout(Ec) (element t + Lc j, as the spectrum rows are loaded), the forward schedule Ec ... Rz
+//     leaves the frequencies in layout(Rz), where the Wiener factor is applied; the inverse schedule
+//     Rz ... Ec returns them.
+// Power-of-two lengths get the plans of fft_core.hpp's RowCfg (natural layout, same arithmetic), so
+// a power-of-two W with a smooth H (or the reverse) runs here too.
+// Inference only (the training forward and backward of these sizes run on the generic kernels).
+#pragma once
+#include "admm_kernels.hpp"
+#include "mixed_fft.hpp"
+
+namespace admm {
+
+// ---------------------------------------------------------------------------------------------
+// plans
+// ---------------------------------------------------------------------------------------------
+// The edge stage of radix R over L lanes leaves element t + L q + (N/R) k in register q + Q k
+// (Q = ceil(N/(R L))): that is the natural layout over Lx lanes (element t + Lx j in register j) when
+// it runs one butterfly per lane over exactly Lx = N/R lanes, or full rows of butterflies over all L
+// lanes (the power-of-two plans: Q = E / R).
+template <int N, int L> __host__ __device__ constexpr bool edge_ok(int R, int Lx) {
+    return ((N / R + L - 1) / L == 1 && N / R == Lx) || (L == Lx && (N / R) % L == 0);
+}
+template <int N> struct MRow;
+// power-of-two rows: fft_core's configuration
+template <int N> struct MRowPow2 {
+    static constexpr int Lg = N / RowCfg<N>::E, Lp = Lg, Ls = Lg, Ep = RowCfg<N>::E, Es = Ep;
+    using Inv = typename RowCfg<N>::S;
+    using Fwd = typename RowCfg<N>::S;
+};
+template <> struct MRow<16> : MRowPow2<16> {};
+template <> struct MRow<32> : MRowPow2<32> {};
+template <> struct MRow<64> : MRowPow2<64> {};
+template <> struct MRow<128> : MRowPow2<128> {};
+template <> struct MRow<256> : MRowPow2<256> {};
+template <> struct MRow<512> : MRowPow2<512> {};
+template <> struct MRow<1024> : MRowPow2<1024> {};
+// smooth rows
+template <> struct MRow<960> {  // W = 1920 (HD)
+    static constexpr int Lg = 64, Lp = 64, Ep = 15, Ls = 60, Es = 16;
+    using Inv = Sched<16, 4, 15>;
+    using Fwd = Sched<15, 4, 16>;
+};
+template <> struct MRow<640> {  // W = 1280 (720p)
+    static constexpr int Lg = 64, Lp = 64, Ep = 10, Ls = 40, Es = 16;
+    using Inv = Sched<16, 4, 10>;
+    using Fwd = Sched<10, 4, 16>;
+};
+template <> struct MRow<480> {  // W = 960
+    static constexpr int Lg = 32, Lp = 32, Ep = 15, Ls = 30, Es = 16;
+    using Inv = Sched<16, 2, 15>;
+    using Fwd = Sched<15, 2, 16>;
+};
+template <> struct MRow<320> {  // W = 640 (VGA)
+    static constexpr int Lg = 32, Lp = 32, Ep = 10, Ls = 20, Es = 16;
+    using Inv = Sched<16, 2, 10>;
+    using Fwd = Sched<10, 2, 16>;
+};
+template <> struct MRow<240> {  // W = 480
+    static constexpr int Lg = 16, Lp = 16, Ep = 15, Ls = 15, Es = 16;
+    using Inv = Sched<16, 15>;
+    using Fwd = Sched<15, 16>;
+};
+template <> struct MRow<360> {  // W = 720
+    static constexpr int Lg = 32, Lp = 24, Ep = 15, Ls = 30, Es = 12;
+    using Inv = Sched<12, 2, 15>;
+    using Fwd = Sched<15, 2, 12>;
+};
+template <> struct MRow<540> {  // W = 1080
+    static constexpr int Lg = 64, Lp = 36, Ep = 15, Ls = 60, Es = 9;
+    using Inv = Sched<9, 4, 15>;
+    using Fwd = Sched<15, 4, 9>;
+};
+
+template <int N> struct MRowG {
+    using P = MRow<N>;
+    static constexpr int Lg = P::Lg, Lp = P::Lp, Ep = P::Ep, Ls = P::Ls, Es = P::Es, W = 2 * N;
+    static constexpr int a = sched_regs<N, Lg>(typename P::Inv{}), b = sched_regs<N, Lg>(typename P::Fwd{});
+    static constexpr int EM = a > b ? a : b;
+    static constexpr int NT = 256, SG = NT / Lg;
+    static_assert(Lp * Ep == N && Ls * Es == N && Lp <= Lg && Ls <= Lg && Lg <= 64 && (Lg & (Lg - 1)) == 0,
+                  "row plan");
+    static_assert(sched_prod(typename P::Inv{}) == N && sched_prod(typename P::Fwd{}) == N, "row schedule");
+    static_assert(edge_ok<N, Lg>(sched_first(typename P::Inv{}), Ls) && edge_ok<N, Lg>(sched_last(typename P::Inv{}), Lp),
+                  "inverse edges");
+    static_assert(edge_ok<N, Lg>(sched_first(typename P::Fwd{}), Lp) && edge_ok<N, Lg>(sched_last(typename P::Fwd{}), Ls),
+                  "forward edges");
+    static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * RowBuf::slots(N)); }
+};
+
+template <int H> struct MCol;
+template <int H> struct MColPow2 {
+    static constexpr int Lc = H / RowCfg<H>::E, Ec = RowCfg<H>::E, C = Lc <= 64 ? 8 : Lc == 128 ? 8 : 4;
+    using Fwd = typename RowCfg<H>::S;
+    using Inv = typename RowCfg<H>::S;
+};
+template <> struct MCol<16> : MColPow2<16> {};
+template <> struct MCol<32> : MColPow2<32> {};
+template <> struct MCol<64> : MColPow2<64> {};
+template <> struct MCol<128> : MColPow2<128> {};
+template <> struct MCol<256> : MColPow2<256> {};
+template <> struct MCol<512> : MColPow2<512> {};
+template <> struct MCol<1024> : MColPow2<1024> {};
+template <> struct MCol<2048> : MColPow2<2048> {};
+template <> struct MCol<4096> : MColPow2<4096> {};
+template <> struct MCol<1080> {
+    static constexpr int Lc = 120, Ec = 9, C = 4;
+    using Fwd = Sched<9, 15, 8>;
+    using Inv = Sched<8, 15, 9>;
+};
+template <> struct MCol<2160> {
+    static constexpr int Lc = 240, Ec = 9, C = 2;
+    using Fwd = Sched<9, 16, 15>;
+    using Inv = Sched<15, 16, 9>;
+};
+template <> struct MCol<720> {
+    static constexpr int Lc = 80, Ec = 9, C = 4;
+    using Fwd = Sched<9, 16, 5>;
+    using Inv = Sched<5, 16, 9>;
+};
+template <> struct MCol<960> {
+    static constexpr int Lc = 64, Ec = 15, C = 8;
+    using Fwd = Sched<15, 16, 4>;
+    using Inv = Sched<4, 16, 15>;
+};
+template <> struct MCol<540> {
+    static constexpr int Lc = 60, Ec = 9, C = 4;
+    using Fwd = Sched<9, 12, 5>;
+    using Inv = Sched<5, 12, 9>;
+};
+template <> struct MCol<480> {
+    static constexpr int Lc = 32, Ec = 15, C = 8;
+    using Fwd = Sched<15, 16, 2>;
+    using Inv = Sched<2, 16, 15>;
+};
+template <> struct MCol<360> {
+    static constexpr int Lc = 40, Ec = 9, C = 8;
+    using Fwd = Sched<9, 8, 5>;
+    using Inv = Sched<5, 8, 9>;
+};
+template <> struct MCol<240> {
+    static constexpr int Lc = 16, Ec = 15, C = 8;
+    using Fwd = Sched<15, 16>;
+    using Inv = Sched<16, 15>;
+};
+
+template <int H> struct MColG {
+    using P = MCol<H>;
+    static constexpr int Lc = P::Lc, Ec = P::Ec, C = P::C, NT = C * Lc;
+    static constexpr int Rz = sched_last(typename P::Fwd{});
+    static constexpr int NBz = H / Rz, Qz = (NBz + Lc - 1) / Lc;
+    static constexpr int a = sched_regs<H, Lc>(typename P::Fwd{}), b = sched_regs<H, Lc>(typename P::Inv{});
+    static constexpr int EM = a > b ? a : b;
+    static_assert(Lc * Ec == H && NT <= 1024, "column plan");
+    static_assert(sched_prod(typename P::Fwd{}) == H && sched_prod(typename P::Inv{}) == H, "column schedule");
+    static_assert(edge_ok<H, Lc>(sched_first(typename P::Fwd{}), Lc) && edge_ok<H, Lc>(sched_last(typename P::Inv{}), Lc),
+                  "column edges");
+    // the inverse starts from the layout the forward ends in (the same radix, or both natural)
+    static_assert(sched_first(typename P::Inv{}) == Rz ||
+                      (NBz % Lc == 0 && (H / sched_first(typename P::Inv{})) % Lc == 0), "column frequency layout");
+    static constexpr size_t lds_bytes() { return sizeof(cf) * (H + (size_t)H * C); }
+};
+
+// ---------------------------------------------------------------------------------------------
+// packed real-row transforms over one row group (as RowXf<N>, admm_kernels.hpp, in the plan's layouts)
+// ---------------------------------------------------------------------------------------------
+template <int N> struct RowXfM {
+    using G = MRowG<N>;
+    static constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM;
+
+    // The Hermitian combine of element k = t + Ls j with its partner N - k, which sits in lane
+    // Ls - t, register Es - 1 - j (t = 0: this lane, register Es - j).  Registers j and Es - 1 - j are
+    // each other's partner registers, so they are combined as a pair from one pair of shuffles (no
+    // partner array held across the loop).
+    template <bool INV>
+    __device__ __forceinline__ static void combine(cf (&v)[EM], const cf* __restrict__ tw, int t) {
+        const int src = (t == 0 || t >= Ls) ? 0 : Ls - t;
+        auto one = [&](int j, cf x, cf pp) -> cf {
+            const int k = t + Ls * j;
+            const cf w = tw[k < N ? k : 0];
+            const cf pc = cconj(pp);
+            if (INV) {  // c2r: e + i o, o = (x - conj p) exp(+2 pi i k / W)
+                const cf e = cadd(x, pc);
+                const cf o = cmulc(csub(x, pc), w);
+                return mkc(e.x - o.y, e.y + o.x);
+            } else {    // r2c: s - i d, d = (x - conj p) exp(-2 pi i k / W)
+                const cf sm = cadd(x, pc);
+                const cf d = cmul(csub(x, pc), w);
+                return mkc(sm.x + d.y, sm.y - d.x);
+            }
+        };
+        // Lane 0's partners are its own registers Es - j, which the loop has already rewritten (as the
+        // previous iteration's jp) by the time it needs them: their original values are carried in prev.
+        const cf v0 = v[0];
+        cf prev = v0;
+#pragma unroll
+        for (int j = 0; j < (Es + 1) / 2; ++j) {
+            const int jp = Es - 1 - j;
+            const cf a = mkc(__shfl(v[jp].x, src, Lg), __shfl(v[jp].y, src, Lg));  // partner of j
+            const cf b = mkc(__shfl(v[j].x, src, Lg), __shfl(v[j].y, src, Lg));    // partner of jp
+            const cf xj = v[j], xp = v[jp];
+            // lane 0: partner of register j is its register Es - j (j = 0: itself), of jp register j + 1
+            const cf pa = t == 0 ? (j == 0 ? v0 : prev) : a;
+            const cf pb = t == 0 ? v[(j + 1) % Es] : b;
+            cf nj = one(j, xj, pa);
+            const cf np = one(jp, xp, pb);
+            if (j == 0 && t == 0)
+                nj = INV ? mkc(v0.x + v0.y, v0.x - v0.y) : mkc(2.f * (v0.x + v0.y), 2.f * (v0.x - v0.y));
+            prev = xp;
+            v[j] = nj;
+            if (jp != j) v[jp] = np;
+        }
+    }
+    // row spectrum in layout(Es) (v[j], j < Es) -> pixel pairs in layout(Ep) (v[j], j < Ep), x 2W
+    __device__ __forceinline__ static void c2r(cf (&v)[EM], const RowBuf& buf, const cf* __restrict__ tw, int t) {
+        combine<true>(v, tw, t);
+        mfft<N, Lg, EM, +1, 0, 2>(v, buf, tw, t, typename MRow<N>::Inv{});
+    }
+    // pixel pairs in layout(Ep) -> packed spectrum (2 rfft) in layout(Es)
+    __device__ __forceinline__ static void r2c(cf (&v)[EM], const RowBuf& buf, const cf* __restrict__ tw, int t) {
+        mfft<N, Lg, EM, -1, 0, 2>(v, buf, tw, t, typename MRow<N>::Fwd{});
+        combine<false>(v, tw, t);
+    }
+};
+
+// real rows (pixel order) -> packed row spectra
+template <int N>
+__global__ void __launch_bounds__(256) k_row_r2c_m(const float* __restrict__ img, cf* __restrict__ spec,
+                                                   const cf* __restrict__ twW_g, long long rows) {
+    using G = MRowG<N>;
+    constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, twW_g, G::W);
+    __syncthreads();
+    const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
+    const long long row = (long long)blockIdx.x * G::SG + sgl;
+    if (row >= rows) return;
+    RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
+    const cf* src = reinterpret_cast<const cf*>(img + row * G::W);
+    cf v[EM];
+    if (t < Lp) {
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) v[j] = src[t + Lp * j];
+    }
+    RowXfM<N>::r2c(v, buf, tw, t);
+    if (t < Ls) {
+        cf* dst = spec + row * N;
+#pragma unroll
+        for (int j = 0; j < Es; ++j) dst[t + Ls * j] = v[j];
+    }
+}
+
+// packed row spectra -> real rows (pixel order)
+template <int N>
+__global__ void __launch_bounds__(256) k_row_c2r_m(const cf* __restrict__ spec, float* __restrict__ img,
+                                                   const cf* __restrict__ twW_g, long long rows) {
+    using G = MRowG<N>;
+    constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, twW_g, G::W);
+    __syncthreads();
+    const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
+    const long long row = (long long)blockIdx.x * G::SG + sgl;
+    if (row >= rows) return;
+    RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
+    const cf* src = spec + row * N;
+    cf v[EM];
+    if (t < Ls) {
+#pragma unroll
+        for (int j = 0; j < Es; ++j) v[j] = src[t + Ls * j];
+    }
+    RowXfM<N>::c2r(v, buf, tw, t);
+    if (t < Lp) {
+        cf* dst = reinterpret_cast<cf*>(img + row * G::W);
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) dst[t + Lp * j] = v[j];
+    }
+}
+
+// Wiener factor for the mixed column pass: fcM[ky][kx] = fcT[kx][ky] / 2 (kx in [0, N], row-major so a
+// block's C adjacent columns read adjacent factors; the / 2 turns the generic path's 1/(HW) scale into
+// the packed row transforms' 1/(2HW), exactly)
+static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restrict__ fcM, int H, int N) {
+    const long long n = (long long)H * (N + 1);
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const int ky = (int)(i / (N + 1)), kx = (int)(i % (N + 1));
+        fcM[i] = 0.5f * fcT[(size_t)kx * H + ky];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass B: column FFT -> Wiener factor -> column IFFT, in place, C columns per block
+// ---------------------------------------------------------------------------------------------
+template <int H>
+__global__ void __launch_bounds__(MColG<H>::NT) k_pass_b_m(cf* spec, const float* __restrict__ fcM,
+                                                           const cf* __restrict__ twH_g, int N, int colblocks,
+                                                           int order) {
+    using G = MColG<H>;
+    constexpr int Lc = G::Lc, Ec = G::Ec, C = G::C, EM = G::EM, NBz = G::NBz, Qz = G::Qz;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* data = tw + H;
+    load_tw(tw, twH_g, H);
+    const int tid = threadIdx.x;
+    const int c = tid % C, t = tid / C;
+    int p, cb;
+    pb_tile(xcd_remap(blockIdx.x, gridDim.x), colblocks, order, true, p, cb);
+    const int col = cb * C + c;
+    const rsrc_t rs = make_rsrc(spec + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
+    const int voff = (t * N + col) * (int)sizeof(cf);
+    const int sstep = Lc * N * (int)sizeof(cf);
+    ColBuf<C> buf{data + c};
+    cf v[EM];
+#pragma unroll
+    for (int j = 0; j < Ec; ++j) v[j] = bload_cf(rs, voff, j * sstep);
+    __syncthreads();  // twiddles in LDS
+    mfft<H, Lc, EM, -1, 1, 1>(v, buf, tw, t, typename MCol<H>::Fwd{});
+    // frequencies in layout(Rz): v[q + Qz k] <-> ky = t + Lc q + NBz k (valid for t + Lc q < NBz)
+    float m[EM];
+#pragma unroll
+    for (int q = 0; q < Qz; ++q) {
+        const int vt = t + Lc * q;
+#pragma unroll
+        for (int k = 0; k < G::Rz; ++k) m[q + Qz * k] = (vt < NBz) ? fcM[(size_t)(vt + NBz * k) * (N + 1) + col] : 0.f;
+    }
+    if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H - ky]
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < Qz; ++q) {
+            const int vt = t + Lc * q;
+            if (vt < NBz) {
+#pragma unroll
+                for (int k = 0; k < G::Rz; ++k) buf.at(vt + NBz * k) = v[q + Qz * k];
+            }
+        }
+        __syncthreads();
+        if (col == 0) {
+#pragma unroll
+            for (int q = 0; q < Qz; ++q) {
+                const int vt = t + Lc * q;
+                if (vt < NBz) {
+#pragma unroll
+                    for (int k = 0; k < G::Rz; ++k) {
+                        const int ky = vt + NBz * k;
+                        const cf qv = cconj(buf.at(ky == 0 ? 0 : H - ky));
+                        const float f0 = m[q + Qz * k], fn = fcM[(size_t)ky * (N + 1) + N];
+                        const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
+                        const cf x = v[q + Qz * k];
+                        v[q + Qz * k] = mkc(fmaf(a, x.x, b * qv.x), fmaf(a, x.y, b * qv.y));
+                    }
+                }
+            }
+        }
+        __syncthreads();  // the partner reads are done before the inverse transform reuses buf
+    }
+    if (col != 0) {
+#pragma unroll
+        for (int i = 0; i < Qz * G::Rz; ++i) v[i] = cscale(v[i], m[i]);
+    }
+    mfft<H, Lc, EM, +1, 1, 1>(v, buf, tw, t, typename MCol<H>::Inv{});
+#pragma unroll
+    for (int j = 0; j < Ec; ++j) bstore_cf(rs, voff, j * sstep, v[j]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass A: the fused row pass (k_pass_a, pixel-order images), one row group per strip of R rows
+// ---------------------------------------------------------------------------------------------
+// occupancy target of the mixed row pass (waves per SIMD): 2 up to 8 pixel pairs per lane, 1 above
+// (15 pairs per lane hold ~4 x 30 VGPRs of row state next to the transform's 32 -- as the power-of-two
+// pass A at W = 2048)
+#ifndef PASSA_M_MINW
+#define PASSA_M_MINW(ep) ((ep) > 8 ? 1 : 2)
+#endif
+template <int N, bool ISO, bool FIRST>
+__global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(PassAArgs a) {
+    using G = MRowG<N>;
+    constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
+    constexpr bool kSpecNT = (ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512);
+    constexpr bool kUNT = (ADMM_NT & 16) != 0;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, a.twW, W);
+    __syncthreads();
+    const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
+    const long long strip = (long long)blockIdx.x * G::SG + sgl;
+    if (strip >= a.nstrips) return;
+    const int H = a.H, R = a.R;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    const float rho = a.rho[0];
+    const float tau = a.lam[0] / rho;
+    const bool pa = t < Lp, sa = t < Ls;  // lane holds pixels / spectrum elements
+    const int lft = t == 0 ? Lp - 1 : t - 1, rgt = t + 1 >= Lp ? 0 : t + 1;  // neighbouring pixel lanes
+
+    const cf* sp = a.sin + (size_t)p * H * N;
+    cf* so = a.sout + (size_t)p * H * N;
+    const size_t poff = (size_t)p * H * W;
+    const cf* bimg = reinterpret_cast<const cf*>(a.b + poff);
+    const cf* uxi = reinterpret_cast<const cf*>(a.uxi + poff);
+    const cf* uyi = reinterpret_cast<const cf*>(a.uyi + poff);
+    cf* uxo = reinterpret_cast<cf*>(a.uxo + poff);
+    cf* uyo = reinterpret_cast<cf*>(a.uyo + poff);
+    const cf* nsx = reinterpret_cast<const cf*>(a.nsq);
+    const cf* nsy = reinterpret_cast<const cf*>(a.nsq + (size_t)H * W);
+
+    // row g's x in pixel layout (spectrum row -> c2r)
+    auto xrow = [&](int g, cf (&x)[Ep]) {
+        cf v[EM];
+        if (sa) {
+#pragma unroll
+            for (int j = 0; j < Es; ++j) v[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + Ls * j]);
+        }
+        RowXfM<N>::c2r(v, buf, tw, t);
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) x[j] = v[j];
+    };
+    cf xprev[Ep], xcur[Ep], wxp[Ep], wyp[Ep];
+    xrow(i0 == 0 ? H - 1 : i0 - 1, xprev);
+    for (int rr = 0; rr <= R; ++rr) {
+        const int g = i0 + rr >= H ? i0 + rr - H : i0 + rr;
+        const size_t ro = (size_t)g * N;  // row offset in cf units (spectrum and pixel pairs alike)
+        xrow(g, xcur);
+
+        // ---- y direction: a_y = x[g] - x[g-1] + u_y; z_y, u_y, w_y of row g
+        cf wyc[Ep];
+        {
+            cf uy[Ep], fy[Ep];
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                uy[j] = (FIRST || !pa) ? mkc(0.f, 0.f) : ld_pol<kUNT>(&uyi[ro + t + Lp * j]);
+                if constexpr (ISO) fy[j] = pa ? nsy[ro + t + Lp * j] : mkc(0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                const float a0 = (xcur[j].x - xprev[j].x) + uy[j].x;
+                const float a1 = (xcur[j].y - xprev[j].y) + uy[j].y;
+                const float z0 = shrink_z<ISO>(a0, tau, ISO ? fy[j].x : 0.f);
+                const float z1 = shrink_z<ISO>(a1, tau, ISO ? fy[j].y : 0.f);
+                const float n0 = a0 - z0, n1 = a1 - z1;  // u_y(new)
+                uy[j] = mkc(n0, n1);
+                wyc[j] = mkc(z0 - n0, z1 - n1);
+            }
+            if (rr < R && pa) {
+#pragma unroll
+                for (int j = 0; j < Ep; ++j) sta(&uyo[ro + t + Lp * j], uy[j]);
+            }
+        }
+
+        // ---- finalize row g-1: v = Dx^T w_x + Dy^T w_y, r = b + rho v, row FFT
+        if (rr >= 1) {
+            const int gm = g == 0 ? H - 1 : g - 1;
+            const size_t rm = (size_t)gm * N;
+            cf sh[Ep];
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) sh[j].x = __shfl(wxp[j].x, rgt, Lg);
+            cf r[EM];
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                const float wr = (t == Lp - 1) ? sh[(j + 1) % Ep].x : sh[j].x;  // w_x at pixel q1+1
+                const cf bb = pa ? lda<16>(&bimg[rm + t + Lp * j]) : mkc(0.f, 0.f);
+                const float v0 = (wxp[j].x - wxp[j].y) + (wyp[j].x - wyc[j].x);
+                const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
+                r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
+            }
+            RowXfM<N>::r2c(r, buf, tw, t);
+            if (sa) {
+#pragma unroll
+                for (int j = 0; j < Es; ++j) sta(&so[rm + t + Ls * j], r[j]);
+            }
+        }
+
+        // ---- x direction: a_x = x[g][j] - x[g][j-1] + u_x; z_x, u_x, w_x of row g
+        if (rr < R) {
+            cf ux[Ep], fx[Ep], sh[Ep];
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                ux[j] = (FIRST || !pa) ? mkc(0.f, 0.f) : ld_pol<kUNT>(&uxi[ro + t + Lp * j]);
+                if constexpr (ISO) fx[j] = pa ? nsx[ro + t + Lp * j] : mkc(0.f, 0.f);
+                sh[j].x = __shfl(xcur[j].y, lft, Lg);
+            }
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                const float xl = (t == 0) ? sh[(j + Ep - 1) % Ep].x : sh[j].x;  // x at pixel q0-1
+                const float a0 = (xcur[j].x - xl) + ux[j].x;
+                const float a1 = (xcur[j].y - xcur[j].x) + ux[j].y;
+                const float z0 = shrink_z<ISO>(a0, tau, ISO ? fx[j].x : 0.f);
+                const float z1 = shrink_z<ISO>(a1, tau, ISO ? fx[j].y : 0.f);
+                const float n0 = a0 - z0, n1 = a1 - z1;
+                ux[j] = mkc(n0, n1);
+                wxp[j] = mkc(z0 - n0, z1 - n1);
+            }
+            if (pa) {
+#pragma unroll
+                for (int j = 0; j < Ep; ++j) sta(&uxo[ro + t + Lp * j], ux[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) {
+            wyp[j] = wyc[j];
+            xprev[j] = xcur[j];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// iso pass A1 (k_iso_norm): per-pixel partial sums over a group of planes of a_x^2, a_y^2
+// ---------------------------------------------------------------------------------------------
+template <int N, bool FIRST>
+__global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
+    using G = MRowG<N>;
+    constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, a.twW, W);
+    __syncthreads();
+    const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
+    const long long item = (long long)blockIdx.x * G::SG + sgl;
+    if (item >= a.nitems) return;
+    const int H = a.H;
+    const int g = (int)(item % H);
+    const int grp = (int)(item / H);
+    const int gm = g == 0 ? H - 1 : g - 1;
+    RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    const bool pa = t < Lp, sa = t < Ls;
+    const int lft = t == 0 ? Lp - 1 : t - 1;
+    cf sx[Ep], sy[Ep];
+#pragma unroll
+    for (int j = 0; j < Ep; ++j) sx[j] = sy[j] = mkc(0.f, 0.f);
+    const int p1 = min(a.P, (grp + 1) * a.ppg);
+    for (int p = grp * a.ppg; p < p1; ++p) {
+        const cf* sp = a.sin + (size_t)p * H * N;
+        cf vp[EM], vc[EM];
+        if (sa) {
+#pragma unroll
+            for (int j = 0; j < Es; ++j) {
+                vp[j] = sp[(size_t)gm * N + t + Ls * j];
+                vc[j] = sp[(size_t)g * N + t + Ls * j];
+            }
+        }
+        RowXfM<N>::c2r(vp, buf, tw, t);
+        RowXfM<N>::c2r(vc, buf, tw, t);
+        const size_t ro = (size_t)p * H * N + (size_t)g * N;  // cf units == pixel pairs
+        const cf* uxi = reinterpret_cast<const cf*>(a.uxi);
+        const cf* uyi = reinterpret_cast<const cf*>(a.uyi);
+        cf sh[Ep];
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) sh[j].x = __shfl(vc[j].y, lft, Lg);
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) {
+            const cf ux = (FIRST || !pa) ? mkc(0.f, 0.f) : uxi[ro + t + Lp * j];
+            const cf uy = (FIRST || !pa) ? mkc(0.f, 0.f) : uyi[ro + t + Lp * j];
+            const float xl = (t == 0) ? sh[(j + Ep - 1) % Ep].x : sh[j].x;
+            const float ax0 = (vc[j].x - xl) + ux.x, ax1 = (vc[j].y - vc[j].x) + ux.y;
+            const float ay0 = (vc[j].x - vp[j].x) + uy.x, ay1 = (vc[j].y - vp[j].y) + uy.y;
+            sx[j].x = fmaf(ax0, ax0, sx[j].x);
+            sx[j].y = fmaf(ax1, ax1, sx[j].y);
+            sy[j].x = fmaf(ay0, ay0, sy[j].x);
+            sy[j].y = fmaf(ay1, ay1, sy[j].y);
+        }
+    }
+    if (pa) {
+        cf* px = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 0) * H * W) + (size_t)g * N;
+        cf* py = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 1) * H * W) + (size_t)g * N;
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) {
+            px[t + Lp * j] = sx[j];
+            py[t + Lp * j] = sy[j];
+        }
+    }
+}
+
+}  // namespace admm
