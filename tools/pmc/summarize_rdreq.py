@@ -17,6 +17,8 @@ import sys
 
 OUT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/rdreq"
 DEST = sys.argv[2] if len(sys.argv) > 2 else None
+# another workload (tools/pmc/run_rdreq_cfg.sh <config>): its pixels per launch, bytes per pixel reported
+CFG_NPX = int(sys.argv[3]) if len(sys.argv) > 3 else None
 NPX = 64 * 3 * 1024 * 1024  # C3 pixels per launch
 ALG = {"pass_a_first": 20 * NPX, "pass_a": 28 * NPX, "pass_b": 8 * NPX}
 
@@ -74,7 +76,10 @@ def main():
     calib = bytes_of(crd, load("calib2")[0], cnl)
     rd, nl = load("bench1")
     kern = bytes_of(rd, load("bench2")[0], nl)
-    rl = roles(kern)
+    rl = roles(kern) if CFG_NPX is None else {}
+    if CFG_NPX:
+        for e in kern.values():
+            e["bytes_per_pixel"] = e["traffic_bytes"] / CFG_NPX
     for role, k in rl.items():
         kern[k]["role"] = role
         kern[k]["algorithmic_bytes"] = ALG[role]
@@ -87,7 +92,8 @@ def main():
                   "32*(TCC_EA0_WRREQ - TCC_EA0_WRREQ_64B), summed over TCC instances, two separate --pmc passes; "
                   "checked on calibration copies of known size. Memory-side requests include Infinity-Cache "
                   "(MALL) hits.",
-        "workload": "bench.py --config c3 (64x3x1024^2, 21x21 PSF, 50 it), 2 steps + 1 warm-up, --no-extras",
+        "workload": ("bench.py --config c3 (64x3x1024^2, 21x21 PSF, 50 it), 2 steps + 1 warm-up, --no-extras"
+                     if CFG_NPX is None else f"tools/pmc/run_rdreq_cfg.sh ({CFG_NPX} pixels per launch), one stream"),
         "build_hash": open(bh).read().strip() if os.path.exists(bh) else None,
         "roles": rl,
         "kernels": {k: e for k, e in kern.items() if e["traffic_bytes"] > 1e4},
@@ -96,7 +102,8 @@ def main():
     for k, e in sorted(summ["kernels"].items(), key=lambda t: -t[1]["traffic_bytes"]):
         print(f"{k[:60]:60s} n={e['launches']:4d} read {e['read_bytes'] / 1e9:7.3f} GB  "
               f"write {e['write_bytes'] / 1e9:7.3f} GB"
-              + (f"  {e['role']}: {e['traffic_over_algorithmic']:.3f} x alg" if "role" in e else ""))
+              + (f"  {e['role']}: {e['traffic_over_algorithmic']:.3f} x alg" if "role" in e else "")
+              + (f"  {e['bytes_per_pixel']:.2f} B/px" if "bytes_per_pixel" in e else ""))
     for k, e in summ["calibration"].items():
         print(f"calib {k[:54]:54s} read {e['read_bytes'] / 1e9:7.3f} GB  write {e['write_bytes'] / 1e9:7.3f} GB")
     with open(os.path.join(OUT, "summary.json"), "w") as f:
