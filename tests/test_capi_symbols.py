@@ -52,12 +52,13 @@ def test_host_entry_points():
     assert lib.admm_tv_abi_version() == 6
     fast, generic = 1, 2
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
-    assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 4096), (8, 64), (1, 1), (481, 321))] == [generic] * 5
+    assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 8192), (8, 64), (1, 1), (481, 321))] == [generic] * 5
     assert [lib.admm_tv_supported(*hw) for hw in ((4097, 16), (5000, 33))] == [generic] * 2  # beyond 4096
     assert [lib.admm_tv_supported(*hw) for hw in ((65537, 16), (16, 70000), (0, 16))] == [0] * 3
     # smooth sizes with transform plans: the fused iteration on mixed-radix transforms (inference)
-    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1920), (720, 1280), (480, 640), (2160, 512))] == [3] * 4
-    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 3840), (1081, 1920), (1080, 1918))] == [generic] * 3
+    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1920), (720, 1280), (480, 640), (2160, 512), (2160, 3840),
+                                                  (1024, 4096), (4096, 4096))] == [3] * 7
+    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 7680), (1081, 1920), (1080, 1918))] == [generic] * 3
     d = _native.desc(64, 3, 1024, 1024, 21, False, 50)
     ws = _native.workspace_size(d)
     img = 64 * 3 * 1024 * 1024 * 4
@@ -161,7 +162,7 @@ def test_supported_sizes():
     from admmtor import _native
     L = _native.load()
     assert L.admm_tv_supported(1024, 1024) == 1 and L.admm_tv_supported(4096, 2048) == 1
-    assert L.admm_tv_supported(15, 17) == 2 and L.admm_tv_supported(4096, 4096) == 2
+    assert L.admm_tv_supported(15, 17) == 2 and L.admm_tv_supported(4096, 4096) == 3
     assert L.admm_tv_supported(6000, 4000) == 2 and L.admm_tv_supported(6800, 16) == 2
     assert L.admm_tv_supported(7680, 4320) == 2 and L.admm_tv_supported(8192, 8192) == 2  # global twiddles
     assert L.admm_tv_supported(10240, 16) == 2 and L.admm_tv_supported(10241, 16) == 2  # global line buffers

@@ -35,24 +35,27 @@ def test_supported_codes():
     from admmtor import _native
     lib = _native.load()
     assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1920), (720, 1280), (480, 640), (2160, 1024), (1024, 960),
-                                                  (540, 1080), (360, 720), (240, 480))] == [3] * 8
+                                                  (540, 1080), (360, 720), (240, 480), (2160, 3840), (4096, 4096))] == [3] * 10
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (4096, 2048))] == [1] * 2
-    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1921), (1080, 3840), (1000, 1920), (481, 321))] == [2] * 4
+    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1921), (1080, 7680), (1000, 1920), (481, 321))] == [2] * 4
 
 
 CASES = [
     # (B, C, H, W), psf, iso, iterations
-    ((1, 3, 1080, 1920), ("gauss:1.5", 9), False, 20),   # HD frame: rows 960 = 16*4*15, columns 1080 = 9*15*8
-    ((2, 3, 720, 1280), ("motion", 15), False, 15),      # 720p: rows 640 = 16*4*10, columns 720 = 9*16*5
-    ((2, 2, 480, 640), ("gauss:1.5", 7), True, 20),      # VGA, iso: rows 320 = 16*2*10 (32-lane groups)
-    ((3, 1, 240, 480), None, True, 12),                  # 16-lane row groups, no PSF
-    ((1, 2, 360, 720), ("motion", 9), False, 10),        # 24 active pixel lanes of 32
-    ((1, 1, 540, 1080), ("gauss:2", 9), True, 10),       # 36 active pixel lanes, 9-point spectrum edge
+    ((1, 3, 1080, 1920), ("gauss:1.5", 9), False, 20),   # HD frame: rows 960 = 8*15*8 (2-wave groups), cols 9*15*8
+    ((2, 3, 720, 1280), ("motion", 15), False, 15),      # 720p: rows 640 = 5*16*8 (2-wave groups), cols 9*16*5
+    ((2, 2, 480, 640), ("gauss:1.5", 7), True, 20),      # VGA, iso: rows 320 = 16*4*5, cols 15*16*2
+    ((3, 1, 240, 480), None, True, 12),                  # 32-lane row groups (30 pixel lanes), no PSF
+    ((1, 2, 360, 720), ("motion", 9), False, 10),        # 45 active pixel lanes of 64
+    ((1, 1, 540, 1080), ("gauss:2", 9), True, 10),       # 9 pixel pairs per lane, 12-point spectrum edge
     ((1, 1, 2160, 1024), ("gauss:2", 11), False, 6),     # power-of-two rows, 2160-point columns (9*16*15)
     ((2, 1, 1024, 960), ("gauss:1.5", 9), False, 8),     # power-of-two columns, 480-point rows
     ((1, 2, 960, 512), None, True, 8),                   # 960-point columns (15*16*4)
     ((1, 1, 1080, 1920), ("random", 5), True, 3),        # iso, non-centrosymmetric PSF, 3 iterations
     ((2, 1, 720, 1280), None, False, 1),                 # one iteration
+    ((1, 1, 2160, 3840), ("gauss:2", 11), False, 5),     # 4K UHD: 4-wave row groups (1920 = 8*15*16), 2160 columns
+    ((1, 1, 4096, 4096), ("gauss:1.5", 9), True, 4),     # 4096-wide power-of-two rows: 4-wave groups (8*4*8*8)
+    ((1, 2, 1080, 2048), None, False, 6),                # 2048-wide rows as 2-wave groups beside 1080 columns
 ]
 
 

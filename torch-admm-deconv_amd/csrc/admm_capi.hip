@@ -111,7 +111,7 @@ int env_int(const char* name, int dflt);
 // are supported_hw).  Inference only: the training forward / backward of these sizes stay generic.
 // ADMM_MIXED=0 (A/B knob) keeps them on the generic kernels.
 bool mixed_hw(int64_t H, int64_t W) {
-    if (supported_hw(H, W) || H < 16 || W < 16 || (W & 1) || H > 4096 || W > 2048) return false;
+    if (supported_hw(H, W) || H < 16 || W < 16 || (W & 1) || H > 4096 || W > 4096) return false;
     if (!admm_mixed::row_ok((int)(W / 2)) || !admm_mixed::col_ok((int)H)) return false;
     return (W / 2) % admm_mixed::col_cols((int)H) == 0 && env_int("ADMM_MIXED", 1) != 0;
 }
@@ -1463,8 +1463,7 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
 }
 
 // rows per strip of the mixed row pass: a divisor of H (8, 4, 2 or 1), halved while there are fewer than
-// ~2 waves per SIMD of strips (the row group of a plan is Lg lanes; rows of 960 and 640 pairs take a
-// whole wave)
+// ~2 waves per SIMD of strips (the row group of a plan is Lg lanes: 16 ... 256)
 int strip_rows_mixed(int H, long long rows, int lanes) {
     int R = 8;
     while (R > 1 && H % R) R /= 2;
@@ -1502,8 +1501,7 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
         }
         if (int e = hchk(admm_mixed::r2c(N, bimg, spec[0], twW, rows, s), "k_row_r2c_m")) return e;  // r_1 = b
     }
-    const int lanes = N >= 640 ? 64 : N >= 320 ? 32 : 16;
-    const int R = strip_rows_mixed(H, rows, lanes);
+    const int R = strip_rows_mixed(H, rows, admm_mixed::row_lanes(N));
     int cur = 0, uin = 0;
     for (int it = 1; it <= d.maxit; ++it) {
         {

@@ -28,6 +28,8 @@ template <class F> hipError_t with_row(int N, F&& f) {
         case 540: return f(std::integral_constant<int, 540>{});
         case 640: return f(std::integral_constant<int, 640>{});
         case 960: return f(std::integral_constant<int, 960>{});
+        case 1920: return f(std::integral_constant<int, 1920>{});
+        case 2048: return f(std::integral_constant<int, 2048>{});
         default: return hipErrorInvalidValue;
     }
 }
@@ -70,6 +72,14 @@ bool row_ok(int N) {
 }
 bool col_ok(int H) {
     return with_col(H, [](auto) { return hipSuccess; }) == hipSuccess;
+}
+int row_lanes(int N) {
+    int l = 0;
+    (void)with_row(N, [&](auto n) {
+        l = MRowG<decltype(n)::value>::Lg;
+        return hipSuccess;
+    });
+    return l;
 }
 int col_cols(int H) {
     int c = 0;

@@ -14,6 +14,7 @@ using admm::cf;
 bool row_ok(int N);
 bool col_ok(int H);
 int col_cols(int H);  // columns per column-pass block (N must be a multiple)
+int row_lanes(int N);  // lanes of a row group (up to 256: several waves)
 
 hipError_t r2c(int N, const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s);
 hipError_t c2r(int N, const cf* spec, float* img, const cf* twW, long long rows, hipStream_t s);

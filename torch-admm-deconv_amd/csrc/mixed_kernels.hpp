@@ -47,42 +47,58 @@ template <> struct MRow<64> : MRowPow2<64> {};
 template <> struct MRow<128> : MRowPow2<128> {};
 template <> struct MRow<256> : MRowPow2<256> {};
 template <> struct MRow<512> : MRowPow2<512> {};
-template <> struct MRow<1024> : MRowPow2<1024> {};
-// smooth rows
-template <> struct MRow<960> {  // W = 1920 (HD)
-    static constexpr int Lg = 64, Lp = 64, Ep = 15, Ls = 60, Es = 16;
-    using Inv = Sched<16, 4, 15>;
-    using Fwd = Sched<15, 4, 16>;
+template <> struct MRow<1024> {  // W = 2048 beside a smooth H: 128 lanes x 8 (2 waves)
+    static constexpr int Lg = 128, Lp = 128, Ep = 8, Ls = 128, Es = 8;
+    using Inv = Sched<8, 16, 8>;
+    using Fwd = Sched<8, 16, 8>;
 };
-template <> struct MRow<640> {  // W = 1280 (720p)
-    static constexpr int Lg = 64, Lp = 64, Ep = 10, Ls = 40, Es = 16;
-    using Inv = Sched<16, 4, 10>;
-    using Fwd = Sched<10, 4, 16>;
+// smooth rows.  Rows whose pixel state would exceed ~8 pairs per lane at 64 lanes run "wide": a row
+// group of 128 or 256 lanes (2 or 4 waves of the block) exchanging through LDS with block barriers, so
+// each lane keeps 8 pixel pairs (15 per lane at 64 lanes measured ~320 VGPRs: 1 wave per SIMD).
+template <> struct MRow<960> {  // W = 1920 (HD): 960 = 8 * 15 * 8 over 120 of 128 lanes
+    static constexpr int Lg = 128, Lp = 120, Ep = 8, Ls = 120, Es = 8;
+    using Inv = Sched<8, 15, 8>;
+    using Fwd = Sched<8, 15, 8>;
 };
-template <> struct MRow<480> {  // W = 960
-    static constexpr int Lg = 32, Lp = 32, Ep = 15, Ls = 30, Es = 16;
-    using Inv = Sched<16, 2, 15>;
-    using Fwd = Sched<15, 2, 16>;
+template <> struct MRow<1920> {  // W = 3840 (4K UHD): spectra 120 x 16, pixels 240 x 8 (4 waves)
+    static constexpr int Lg = 256, Lp = 240, Ep = 8, Ls = 120, Es = 16;
+    using Inv = Sched<16, 15, 8>;
+    using Fwd = Sched<8, 15, 16>;
 };
-template <> struct MRow<320> {  // W = 640 (VGA)
-    static constexpr int Lg = 32, Lp = 32, Ep = 10, Ls = 20, Es = 16;
-    using Inv = Sched<16, 2, 10>;
-    using Fwd = Sched<10, 2, 16>;
+template <> struct MRow<2048> {  // W = 4096: 256 lanes x 8 (4 waves)
+    static constexpr int Lg = 256, Lp = 256, Ep = 8, Ls = 256, Es = 8;
+    using Inv = Sched<8, 4, 8, 8>;
+    using Fwd = Sched<8, 8, 4, 8>;
 };
-template <> struct MRow<240> {  // W = 480
-    static constexpr int Lg = 16, Lp = 16, Ep = 15, Ls = 15, Es = 16;
-    using Inv = Sched<16, 15>;
-    using Fwd = Sched<15, 16>;
+template <> struct MRow<640> {  // W = 1280 (720p): spectra 128 x 5, pixels 80 x 8 (2 waves)
+    static constexpr int Lg = 128, Lp = 80, Ep = 8, Ls = 128, Es = 5;
+    using Inv = Sched<5, 16, 8>;
+    using Fwd = Sched<8, 16, 5>;
 };
-template <> struct MRow<360> {  // W = 720
-    static constexpr int Lg = 32, Lp = 24, Ep = 15, Ls = 30, Es = 12;
-    using Inv = Sched<12, 2, 15>;
-    using Fwd = Sched<15, 2, 12>;
+template <> struct MRow<480> {  // W = 960: spectra 40 x 12, pixels 60 x 8
+    static constexpr int Lg = 64, Lp = 60, Ep = 8, Ls = 40, Es = 12;
+    using Inv = Sched<12, 5, 8>;
+    using Fwd = Sched<8, 5, 12>;
 };
-template <> struct MRow<540> {  // W = 1080
-    static constexpr int Lg = 64, Lp = 36, Ep = 15, Ls = 60, Es = 9;
-    using Inv = Sched<9, 4, 15>;
-    using Fwd = Sched<15, 4, 9>;
+template <> struct MRow<320> {  // W = 640 (VGA): spectra 20 x 16, pixels 64 x 5
+    static constexpr int Lg = 64, Lp = 64, Ep = 5, Ls = 20, Es = 16;
+    using Inv = Sched<16, 4, 5>;
+    using Fwd = Sched<5, 4, 16>;
+};
+template <> struct MRow<240> {  // W = 480: spectra 16 x 15, pixels 30 x 8
+    static constexpr int Lg = 32, Lp = 30, Ep = 8, Ls = 16, Es = 15;
+    using Inv = Sched<15, 2, 8>;
+    using Fwd = Sched<8, 2, 15>;
+};
+template <> struct MRow<360> {  // W = 720: spectra 40 x 9, pixels 45 x 8
+    static constexpr int Lg = 64, Lp = 45, Ep = 8, Ls = 40, Es = 9;
+    using Inv = Sched<9, 5, 8>;
+    using Fwd = Sched<8, 5, 9>;
+};
+template <> struct MRow<540> {  // W = 1080: spectra 45 x 12, pixels 60 x 9
+    static constexpr int Lg = 64, Lp = 60, Ep = 9, Ls = 45, Es = 12;
+    using Inv = Sched<12, 5, 9>;
+    using Fwd = Sched<9, 5, 12>;
 };
 
 template <int N> struct MRowG {
@@ -91,7 +107,9 @@ template <int N> struct MRowG {
     static constexpr int a = sched_regs<N, Lg>(typename P::Inv{}), b = sched_regs<N, Lg>(typename P::Fwd{});
     static constexpr int EM = a > b ? a : b;
     static constexpr int NT = 256, SG = NT / Lg;
-    static_assert(Lp * Ep == N && Ls * Es == N && Lp <= Lg && Ls <= Lg && Lg <= 64 && (Lg & (Lg - 1)) == 0,
+    static constexpr bool WIDE = Lg > 64;  // the row group spans several waves: LDS exchanges, block barriers
+    static constexpr int SYNC = WIDE ? 1 : 0;
+    static_assert(Lp * Ep == N && Ls * Es == N && Lp <= Lg && Ls <= Lg && Lg <= 256 && (Lg & (Lg - 1)) == 0,
                   "row plan");
     static_assert(sched_prod(typename P::Inv{}) == N && sched_prod(typename P::Fwd{}) == N, "row schedule");
     static_assert(edge_ok<N, Lg>(sched_first(typename P::Inv{}), Ls) && edge_ok<N, Lg>(sched_last(typename P::Inv{}), Lp),
@@ -103,7 +121,8 @@ template <int N> struct MRowG {
 
 template <int H> struct MCol;
 template <int H> struct MColPow2 {
-    static constexpr int Lc = H / RowCfg<H>::E, Ec = RowCfg<H>::E, C = Lc <= 64 ? 8 : Lc == 128 ? 8 : 4;
+    // up to 512 threads per block (1,024 would cap the transform at 128 VGPRs: it spills at H >= 2048)
+    static constexpr int Lc = H / RowCfg<H>::E, Ec = RowCfg<H>::E, C = Lc <= 64 ? 8 : 512 / Lc;
     using Fwd = typename RowCfg<H>::S;
     using Inv = typename RowCfg<H>::S;
 };
@@ -180,6 +199,43 @@ template <int H> struct MColG {
 template <int N> struct RowXfM {
     using G = MRowG<N>;
     static constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM;
+    static constexpr bool WIDE = G::WIDE;
+    static constexpr int SYNC = G::SYNC;
+
+    template <bool INV> __device__ __forceinline__ static cf one(int k, cf x, cf pp, const cf* __restrict__ tw) {
+        const cf w = tw[k < N ? k : 0];
+        const cf pc = cconj(pp);
+        if (INV) {  // c2r: e + i o, o = (x - conj p) exp(+2 pi i k / W)
+            const cf e = cadd(x, pc);
+            const cf o = cmulc(csub(x, pc), w);
+            return mkc(e.x - o.y, e.y + o.x);
+        } else {    // r2c: s - i d, d = (x - conj p) exp(-2 pi i k / W)
+            const cf sm = cadd(x, pc);
+            const cf d = cmul(csub(x, pc), w);
+            return mkc(sm.x + d.y, sm.y - d.x);
+        }
+    }
+    // wide row groups: the partners through the LDS exchange buffer (every lane of the block takes part)
+    template <bool INV>
+    __device__ __forceinline__ static void combine_lds(cf (&v)[EM], const RowBuf& buf, const cf* __restrict__ tw, int t) {
+        xsync<1>();
+        if (t < Ls) {
+#pragma unroll
+            for (int j = 0; j < Es; ++j) buf.at(t + Ls * j) = v[j];
+        }
+        xsync<1>();
+#pragma unroll
+        for (int j = 0; j < Es; ++j) {
+            const int k = t + Ls * j;
+            const cf x = v[j];
+            if (k == 0) {
+                v[j] = INV ? mkc(x.x + x.y, x.x - x.y) : mkc(2.f * (x.x + x.y), 2.f * (x.x - x.y));
+            } else {
+                const int kp = N - k;
+                v[j] = one<INV>(k, x, buf.at(kp >= 0 ? kp : 0), tw);
+            }
+        }
+    }
 
     // The Hermitian combine of element k = t + Ls j with its partner N - k, which sits in lane
     // Ls - t, register Es - 1 - j (t = 0: this lane, register Es - j).  Registers j and Es - 1 - j are
@@ -188,20 +244,7 @@ template <int N> struct RowXfM {
     template <bool INV>
     __device__ __forceinline__ static void combine(cf (&v)[EM], const cf* __restrict__ tw, int t) {
         const int src = (t == 0 || t >= Ls) ? 0 : Ls - t;
-        auto one = [&](int j, cf x, cf pp) -> cf {
-            const int k = t + Ls * j;
-            const cf w = tw[k < N ? k : 0];
-            const cf pc = cconj(pp);
-            if (INV) {  // c2r: e + i o, o = (x - conj p) exp(+2 pi i k / W)
-                const cf e = cadd(x, pc);
-                const cf o = cmulc(csub(x, pc), w);
-                return mkc(e.x - o.y, e.y + o.x);
-            } else {    // r2c: s - i d, d = (x - conj p) exp(-2 pi i k / W)
-                const cf sm = cadd(x, pc);
-                const cf d = cmul(csub(x, pc), w);
-                return mkc(sm.x + d.y, sm.y - d.x);
-            }
-        };
+        auto one = [&](int j, cf x, cf pp) -> cf { return RowXfM::one<INV>(t + Ls * j, x, pp, tw); };
         // Lane 0's partners are its own registers Es - j, which the loop has already rewritten (as the
         // previous iteration's jp) by the time it needs them: their original values are carried in prev.
         const cf v0 = v[0];
@@ -226,13 +269,44 @@ template <int N> struct RowXfM {
     }
     // row spectrum in layout(Es) (v[j], j < Es) -> pixel pairs in layout(Ep) (v[j], j < Ep), x 2W
     __device__ __forceinline__ static void c2r(cf (&v)[EM], const RowBuf& buf, const cf* __restrict__ tw, int t) {
-        combine<true>(v, tw, t);
-        mfft<N, Lg, EM, +1, 0, 2>(v, buf, tw, t, typename MRow<N>::Inv{});
+        if constexpr (WIDE) combine_lds<true>(v, buf, tw, t);
+        else combine<true>(v, tw, t);
+        mfft<N, Lg, EM, +1, SYNC, 2>(v, buf, tw, t, typename MRow<N>::Inv{});
     }
     // pixel pairs in layout(Ep) -> packed spectrum (2 rfft) in layout(Es)
     __device__ __forceinline__ static void r2c(cf (&v)[EM], const RowBuf& buf, const cf* __restrict__ tw, int t) {
-        mfft<N, Lg, EM, -1, 0, 2>(v, buf, tw, t, typename MRow<N>::Fwd{});
-        combine<false>(v, tw, t);
+        mfft<N, Lg, EM, -1, SYNC, 2>(v, buf, tw, t, typename MRow<N>::Fwd{});
+        if constexpr (WIDE) combine_lds<false>(v, buf, tw, t);
+        else combine<false>(v, tw, t);
+    }
+    // the value of pixel-pair neighbour k + SHIFT (SHIFT = -1 / +1, circular) of every pair this lane
+    // holds: lane shuffles within a wave, the LDS buffer across the waves of a wide row group
+    template <int SHIFT>
+    __device__ __forceinline__ static void neighbour(const float (&val)[Ep], float (&out)[Ep], const RowBuf& buf, int t) {
+        if constexpr (WIDE) {
+            xsync<1>();
+            if (t < Lp) {
+#pragma unroll
+                for (int j = 0; j < Ep; ++j) buf.at(t + Lp * j).x = val[j];
+            }
+            xsync<1>();
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                int k = t + Lp * j + SHIFT;
+                k = k < 0 ? N - 1 : k >= N ? 0 : k;
+                out[j] = buf.at(k).x;
+            }
+        } else {
+            const int src = SHIFT < 0 ? (t == 0 ? Lp - 1 : t - 1) : (t + 1 >= Lp ? 0 : t + 1);
+            float sh[Ep];
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) sh[j] = __shfl(val[j], src, Lg);
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                if (SHIFT < 0) out[j] = (t == 0) ? sh[(j + Ep - 1) % Ep] : sh[j];
+                else out[j] = (t == Lp - 1) ? sh[(j + 1) % Ep] : sh[j];
+            }
+        }
     }
 };
 
@@ -247,8 +321,10 @@ __global__ void __launch_bounds__(256) k_row_r2c_m(const float* __restrict__ img
     load_tw(tw, twW_g, G::W);
     __syncthreads();
     const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
-    const long long row = (long long)blockIdx.x * G::SG + sgl;
-    if (row >= rows) return;
+    long long row = (long long)blockIdx.x * G::SG + sgl;
+    const bool ok = row < rows;
+    if (!G::WIDE && !ok) return;  // (a wide row group keeps every lane for the block barriers)
+    if (!ok) row = rows - 1;
     RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
     const cf* src = reinterpret_cast<const cf*>(img + row * G::W);
     cf v[EM];
@@ -257,7 +333,7 @@ __global__ void __launch_bounds__(256) k_row_r2c_m(const float* __restrict__ img
         for (int j = 0; j < Ep; ++j) v[j] = src[t + Lp * j];
     }
     RowXfM<N>::r2c(v, buf, tw, t);
-    if (t < Ls) {
+    if (ok && t < Ls) {
         cf* dst = spec + row * N;
 #pragma unroll
         for (int j = 0; j < Es; ++j) dst[t + Ls * j] = v[j];
@@ -275,8 +351,10 @@ __global__ void __launch_bounds__(256) k_row_c2r_m(const cf* __restrict__ spec, 
     load_tw(tw, twW_g, G::W);
     __syncthreads();
     const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
-    const long long row = (long long)blockIdx.x * G::SG + sgl;
-    if (row >= rows) return;
+    long long row = (long long)blockIdx.x * G::SG + sgl;
+    const bool ok = row < rows;
+    if (!G::WIDE && !ok) return;
+    if (!ok) row = rows - 1;
     RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
     const cf* src = spec + row * N;
     cf v[EM];
@@ -285,7 +363,7 @@ __global__ void __launch_bounds__(256) k_row_c2r_m(const cf* __restrict__ spec, 
         for (int j = 0; j < Es; ++j) v[j] = src[t + Ls * j];
     }
     RowXfM<N>::c2r(v, buf, tw, t);
-    if (t < Lp) {
+    if (ok && t < Lp) {
         cf* dst = reinterpret_cast<cf*>(img + row * G::W);
 #pragma unroll
         for (int j = 0; j < Ep; ++j) dst[t + Lp * j] = v[j];
@@ -380,11 +458,10 @@ __global__ void __launch_bounds__(MColG<H>::NT) k_pass_b_m(cf* spec, const float
 // ---------------------------------------------------------------------------------------------
 // pass A: the fused row pass (k_pass_a, pixel-order images), one row group per strip of R rows
 // ---------------------------------------------------------------------------------------------
-// occupancy target of the mixed row pass (waves per SIMD): 2 up to 8 pixel pairs per lane, 1 above
-// (15 pairs per lane hold ~4 x 30 VGPRs of row state next to the transform's 32 -- as the power-of-two
-// pass A at W = 2048)
+// occupancy target of the mixed row pass (waves per SIMD): the plans keep <= 9 pixel pairs per lane
+// (wide row groups where a wave would need more), ~150-170 VGPRs: 2 guaranteed, 3 when they fit
 #ifndef PASSA_M_MINW
-#define PASSA_M_MINW(ep) ((ep) > 8 ? 1 : 2)
+#define PASSA_M_MINW(ep) ((ep) > 9 ? 1 : 2)
 #endif
 template <int N, bool ISO, bool FIRST>
 __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(PassAArgs a) {
@@ -397,8 +474,10 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
     load_tw(tw, a.twW, W);
     __syncthreads();
     const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
-    const long long strip = (long long)blockIdx.x * G::SG + sgl;
-    if (strip >= a.nstrips) return;
+    long long strip = (long long)blockIdx.x * G::SG + sgl;
+    const bool ok = strip < a.nstrips;  // a wide row group past the last strip redoes it without storing
+    if (!G::WIDE && !ok) return;
+    if (!ok) strip = a.nstrips - 1;
     const int H = a.H, R = a.R;
     const int spp = H / R;
     const long long p = strip / spp;
@@ -407,7 +486,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
     const float rho = a.rho[0];
     const float tau = a.lam[0] / rho;
     const bool pa = t < Lp, sa = t < Ls;  // lane holds pixels / spectrum elements
-    const int lft = t == 0 ? Lp - 1 : t - 1, rgt = t + 1 >= Lp ? 0 : t + 1;  // neighbouring pixel lanes
+    const bool pst = ok && pa, sst = ok && sa;  // ... and stores them
 
     const cf* sp = a.sin + (size_t)p * H * N;
     cf* so = a.sout + (size_t)p * H * N;
@@ -457,7 +536,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
                 uy[j] = mkc(n0, n1);
                 wyc[j] = mkc(z0 - n0, z1 - n1);
             }
-            if (rr < R && pa) {
+            if (rr < R && pst) {
 #pragma unroll
                 for (int j = 0; j < Ep; ++j) sta(&uyo[ro + t + Lp * j], uy[j]);
             }
@@ -467,20 +546,21 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
         if (rr >= 1) {
             const int gm = g == 0 ? H - 1 : g - 1;
             const size_t rm = (size_t)gm * N;
-            cf sh[Ep];
+            float wxs[Ep], wrs[Ep];
 #pragma unroll
-            for (int j = 0; j < Ep; ++j) sh[j].x = __shfl(wxp[j].x, rgt, Lg);
+            for (int j = 0; j < Ep; ++j) wxs[j] = wxp[j].x;
+            RowXfM<N>::template neighbour<+1>(wxs, wrs, buf, t);  // w_x at pixel q1+1
             cf r[EM];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
-                const float wr = (t == Lp - 1) ? sh[(j + 1) % Ep].x : sh[j].x;  // w_x at pixel q1+1
+                const float wr = wrs[j];
                 const cf bb = pa ? lda<16>(&bimg[rm + t + Lp * j]) : mkc(0.f, 0.f);
                 const float v0 = (wxp[j].x - wxp[j].y) + (wyp[j].x - wyc[j].x);
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
                 r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
             }
             RowXfM<N>::r2c(r, buf, tw, t);
-            if (sa) {
+            if (sst) {
 #pragma unroll
                 for (int j = 0; j < Es; ++j) sta(&so[rm + t + Ls * j], r[j]);
             }
@@ -488,16 +568,18 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
 
         // ---- x direction: a_x = x[g][j] - x[g][j-1] + u_x; z_x, u_x, w_x of row g
         if (rr < R) {
-            cf ux[Ep], fx[Ep], sh[Ep];
+            cf ux[Ep], fx[Ep];
+            float xys[Ep], xls[Ep];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
                 ux[j] = (FIRST || !pa) ? mkc(0.f, 0.f) : ld_pol<kUNT>(&uxi[ro + t + Lp * j]);
                 if constexpr (ISO) fx[j] = pa ? nsx[ro + t + Lp * j] : mkc(0.f, 0.f);
-                sh[j].x = __shfl(xcur[j].y, lft, Lg);
+                xys[j] = xcur[j].y;
             }
+            RowXfM<N>::template neighbour<-1>(xys, xls, buf, t);  // x at pixel q0-1
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
-                const float xl = (t == 0) ? sh[(j + Ep - 1) % Ep].x : sh[j].x;  // x at pixel q0-1
+                const float xl = xls[j];
                 const float a0 = (xcur[j].x - xl) + ux[j].x;
                 const float a1 = (xcur[j].y - xcur[j].x) + ux[j].y;
                 const float z0 = shrink_z<ISO>(a0, tau, ISO ? fx[j].x : 0.f);
@@ -506,7 +588,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
                 ux[j] = mkc(n0, n1);
                 wxp[j] = mkc(z0 - n0, z1 - n1);
             }
-            if (pa) {
+            if (pst) {
 #pragma unroll
                 for (int j = 0; j < Ep; ++j) sta(&uxo[ro + t + Lp * j], ux[j]);
             }
@@ -531,15 +613,16 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
     load_tw(tw, a.twW, W);
     __syncthreads();
     const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
-    const long long item = (long long)blockIdx.x * G::SG + sgl;
-    if (item >= a.nitems) return;
+    long long item = (long long)blockIdx.x * G::SG + sgl;
+    const bool ok = item < a.nitems;
+    if (!G::WIDE && !ok) return;
+    if (!ok) item = a.nitems - 1;
     const int H = a.H;
     const int g = (int)(item % H);
     const int grp = (int)(item / H);
     const int gm = g == 0 ? H - 1 : g - 1;
     RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
     const bool pa = t < Lp, sa = t < Ls;
-    const int lft = t == 0 ? Lp - 1 : t - 1;
     cf sx[Ep], sy[Ep];
 #pragma unroll
     for (int j = 0; j < Ep; ++j) sx[j] = sy[j] = mkc(0.f, 0.f);
@@ -559,14 +642,15 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
         const size_t ro = (size_t)p * H * N + (size_t)g * N;  // cf units == pixel pairs
         const cf* uxi = reinterpret_cast<const cf*>(a.uxi);
         const cf* uyi = reinterpret_cast<const cf*>(a.uyi);
-        cf sh[Ep];
+        float xys[Ep], xls[Ep];
 #pragma unroll
-        for (int j = 0; j < Ep; ++j) sh[j].x = __shfl(vc[j].y, lft, Lg);
+        for (int j = 0; j < Ep; ++j) xys[j] = vc[j].y;
+        RowXfM<N>::template neighbour<-1>(xys, xls, buf, t);
 #pragma unroll
         for (int j = 0; j < Ep; ++j) {
             const cf ux = (FIRST || !pa) ? mkc(0.f, 0.f) : uxi[ro + t + Lp * j];
             const cf uy = (FIRST || !pa) ? mkc(0.f, 0.f) : uyi[ro + t + Lp * j];
-            const float xl = (t == 0) ? sh[(j + Ep - 1) % Ep].x : sh[j].x;
+            const float xl = xls[j];
             const float ax0 = (vc[j].x - xl) + ux.x, ax1 = (vc[j].y - vc[j].x) + ux.y;
             const float ay0 = (vc[j].x - vp[j].x) + uy.x, ay1 = (vc[j].y - vp[j].y) + uy.y;
             sx[j].x = fmaf(ax0, ax0, sx[j].x);
@@ -575,7 +659,7 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
             sy[j].y = fmaf(ay1, ay1, sy[j].y);
         }
     }
-    if (pa) {
+    if (ok && pa) {
         cf* px = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 0) * H * W) + (size_t)g * N;
         cf* py = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 1) * H * W) + (size_t)g * N;
 #pragma unroll
