@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, iso, q, B=5, dt=torch.float32):
+def _worker(rank, world, port, iso, q, B=5, dt=torch.float32, hw=(64, 128)):
     import sys
     import torch.distributed as dist
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -36,7 +36,7 @@ def _worker(rank, world, port, iso, q, B=5, dt=torch.float32):
         from admmtor.synth import blurred_batch, make_psf
         dev = torch.device("cuda:0")
         k = make_psf("motion", 7).to(dev)
-        full = blurred_batch(B, 3, 64, 128, k.cpu(), seed=21).to(dev)
+        full = blurred_batch(B, 3, hw[0], hw[1], k.cpu(), seed=21).to(dev)
         cot = torch.randn(full.shape, generator=torch.Generator().manual_seed(5)).to(dev)
         k, full, cot = k.to(dt), full.to(dt), cot.to(dt)
         s, e = shard_bounds(B, world, rank)
@@ -101,7 +101,7 @@ def _direct_iso(xl, k, lam, rho, maxit):
     return out
 
 
-def _rho_grad_noise(B):
+def _rho_grad_noise(B, hw=(64, 128)):
     """How far the reference formulation's own fp32 rho gradient moves under the reassociation that
     sharding performs: the oracle's restatement (CPU) in fp32 with the batch in four orders -- the
     per-pixel norm (deconv.py:23-24) then sums the same (B, C) terms in another order -- each against
@@ -113,7 +113,7 @@ def _rho_grad_noise(B):
     from admmtor.synth import blurred_batch, make_psf
     from oracle.admm_oracle import solve_fourier
     k = make_psf("motion", 7)
-    full = blurred_batch(B, 3, 64, 128, k, seed=21)
+    full = blurred_batch(B, 3, hw[0], hw[1], k, seed=21)
     cot = torch.randn(full.shape, generator=torch.Generator().manual_seed(5))
 
     def grad(dt, order):
@@ -127,24 +127,28 @@ def _rho_grad_noise(B):
     return max(abs(grad(torch.float32, o) - g64) / abs(g64) for o in orders)
 
 
-@pytest.mark.parametrize("world,iso,B,f64", [(2, False, 5, False), (2, True, 5, False), (2, True, 1, False),
-                                             (8, False, 16, False), (8, True, 11, False), (8, True, 11, True)])
-def test_sharded_world2_on_gpu(cuda_dev, world, iso, B, f64):
+@pytest.mark.parametrize("world,iso,B,f64,hw", [(2, False, 5, False, (64, 128)), (2, True, 5, False, (64, 128)),
+                                                (2, True, 1, False, (64, 128)), (8, False, 16, False, (64, 128)),
+                                                (8, True, 11, False, (64, 128)), (8, True, 11, True, (64, 128)),
+                                                (2, True, 5, False, (240, 480))])
+def test_sharded_world2_on_gpu(cuda_dev, world, iso, B, f64, hw):
     """B = 1 with iso: rank 1's shard is empty and takes part in every all-reduce of the forward
     and the backward with zeros (ABI v4 participate-only call); without that rank 0 would hang.
     world = 8: config 4's topology (BASELINE configs[3]: the batch over 8 ranks, 64 images each),
-    here 16 images (2 per rank) and 11 (uneven shards: 2 2 2 1 1 1 1 1) at a reduced size."""
+    here 16 images (2 per rank) and 11 (uneven shards: 2 2 2 1 1 1 1 1) at a reduced size.
+    240 x 480: a smooth size, whose inference solve (the gathered output) runs the mixed-radix fused
+    kernels with the all-reduce hook and whose training solve the generic kernels."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     dt = torch.float64 if f64 else torch.float32
-    procs = [ctx.Process(target=_worker, args=(r, world, port, iso, q, B, dt)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, iso, q, B, dt, hw)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    noise = _rho_grad_noise(B) if (iso and not f64) else 0.0
+    noise = _rho_grad_noise(B, hw) if (iso and not f64) else 0.0
     if noise:
         print(f"reference-formulation fp32 rho-gradient noise on this input: {noise:.2e}")
     for rank, e_out, e_gx, e_gl, e_gr, bitexact, e_gat, e_side, e_direct in sorted(q.get(timeout=10) for _ in range(world)):

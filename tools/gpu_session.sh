@@ -26,7 +26,7 @@ if [ "$BENCH" = "bench" ]; then
     timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo bench_fail; tail -20 "$OUT/bench.err"; exit 1; }
     echo bench_ok
     head -c 3000 "$OUT/bench.json"; echo
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o prof -- python3 bench.py --steps 5 --warmup 2 \
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o prof -- python3 bench.py --steps 5 --warmup 2 \
         --no-cpu-baseline > "$OUT/bench_rocprof.json" 2> "$OUT/bench_rocprof.err" || { echo rocprof_fail; tail -20 "$OUT/bench_rocprof.err"; exit 1; }
     echo rocprof_ok
 fi

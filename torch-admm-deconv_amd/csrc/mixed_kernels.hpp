@@ -55,15 +55,25 @@ template <> struct MRow<1024> {  // W = 2048 beside a smooth H: 128 lanes x 8 (2
 // smooth rows.  Rows whose pixel state would exceed ~8 pairs per lane at 64 lanes run "wide": a row
 // group of 128 or 256 lanes (2 or 4 waves of the block) exchanging through LDS with block barriers, so
 // each lane keeps 8 pixel pairs (15 per lane at 64 lanes measured ~320 VGPRs: 1 wave per SIMD).
+// ADMM_M960_V (A/B build knob): 0 = 960 as 8 * 15 * 8, 1 = 8 * 3 * 5 * 8 (smaller butterflies, one more
+// exchange)
+#ifndef ADMM_M960_V
+#define ADMM_M960_V 0
+#endif
 template <> struct MRow<960> {  // W = 1920 (HD): 960 = 8 * 15 * 8 over 120 of 128 lanes
     static constexpr int Lg = 128, Lp = 120, Ep = 8, Ls = 120, Es = 8;
+#if ADMM_M960_V == 1
+    using Inv = Sched<8, 3, 5, 8>;
+    using Fwd = Sched<8, 5, 3, 8>;
+#else
     using Inv = Sched<8, 15, 8>;
     using Fwd = Sched<8, 15, 8>;
+#endif
 };
-template <> struct MRow<1920> {  // W = 3840 (4K UHD): spectra 120 x 16, pixels 240 x 8 (4 waves)
-    static constexpr int Lg = 256, Lp = 240, Ep = 8, Ls = 120, Es = 16;
-    using Inv = Sched<16, 15, 8>;
-    using Fwd = Sched<8, 15, 16>;
+template <> struct MRow<1920> {  // W = 3840 (4K UHD): spectra and pixels 240 x 8 (4 waves), 8 * 6 * 5 * 8
+    static constexpr int Lg = 256, Lp = 240, Ep = 8, Ls = 240, Es = 8;
+    using Inv = Sched<8, 6, 5, 8>;
+    using Fwd = Sched<8, 5, 6, 8>;
 };
 template <> struct MRow<2048> {  // W = 4096: 256 lanes x 8 (4 waves)
     static constexpr int Lg = 256, Lp = 256, Ep = 8, Ls = 256, Es = 8;
@@ -101,6 +111,9 @@ template <> struct MRow<540> {  // W = 1080: spectra 45 x 12, pixels 60 x 9
     using Fwd = Sched<9, 5, 12>;
 };
 
+#ifndef ADMM_MIXED_PP
+#define ADMM_MIXED_PP 0
+#endif
 template <int N> struct MRowG {
     using P = MRow<N>;
     static constexpr int Lg = P::Lg, Lp = P::Lp, Ep = P::Ep, Ls = P::Ls, Es = P::Es, W = 2 * N;
@@ -116,7 +129,11 @@ template <int N> struct MRowG {
                   "inverse edges");
     static_assert(edge_ok<N, Lg>(sched_first(typename P::Fwd{}), Lp) && edge_ok<N, Lg>(sched_last(typename P::Fwd{}), Ls),
                   "forward edges");
-    static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * RowBuf::slots(N)); }
+    // ADMM_MIXED_PP (A/B build knob): wide row groups ping-pong between two exchange buffers (one barrier
+    // per exchange) instead of one buffer with a barrier before and after each write
+    static constexpr bool PP = WIDE && ADMM_MIXED_PP != 0;
+    static constexpr int NBUF = PP ? 2 : 1;
+    static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * NBUF * RowBuf::slots(N)); }
 };
 
 template <int H> struct MCol;
@@ -135,8 +152,13 @@ template <> struct MCol<512> : MColPow2<512> {};
 template <> struct MCol<1024> : MColPow2<1024> {};
 template <> struct MCol<2048> : MColPow2<2048> {};
 template <> struct MCol<4096> : MColPow2<4096> {};
+// columns per block of the smooth column plans: 8 (64-byte row segments, pairs of blocks sharing each
+// 128-byte line, as k_pass_b) wherever 8 Lc <= 1024 threads; ADMM_MCOL_C (A/B build knob) overrides
+#ifndef ADMM_MCOL_C
+#define ADMM_MCOL_C 8
+#endif
 template <> struct MCol<1080> {
-    static constexpr int Lc = 120, Ec = 9, C = 4;
+    static constexpr int Lc = 120, Ec = 9, C = ADMM_MCOL_C;
     using Fwd = Sched<9, 15, 8>;
     using Inv = Sched<8, 15, 9>;
 };
@@ -146,7 +168,7 @@ template <> struct MCol<2160> {
     using Inv = Sched<15, 16, 9>;
 };
 template <> struct MCol<720> {
-    static constexpr int Lc = 80, Ec = 9, C = 4;
+    static constexpr int Lc = 80, Ec = 9, C = ADMM_MCOL_C;
     using Fwd = Sched<9, 16, 5>;
     using Inv = Sched<5, 16, 9>;
 };
@@ -156,7 +178,7 @@ template <> struct MCol<960> {
     using Inv = Sched<4, 16, 15>;
 };
 template <> struct MCol<540> {
-    static constexpr int Lc = 60, Ec = 9, C = 4;
+    static constexpr int Lc = 60, Ec = 9, C = ADMM_MCOL_C;
     using Fwd = Sched<9, 12, 5>;
     using Inv = Sched<5, 12, 9>;
 };
@@ -215,15 +237,24 @@ template <int N> struct RowXfM {
             return mkc(sm.x + d.y, sm.y - d.x);
         }
     }
+    // the row group's LDS: one exchange buffer (a single wave), or two used in turn with the exchange
+    // parity ph (wide groups: one barrier per exchange, mixed_fft.hpp mstage_pp)
+    struct Lds {
+        cf* base;  // buffer 0; buffer 1 (wide groups) RowBuf::slots(N) further
+        int ph;
+        __device__ __forceinline__ RowBuf cur() const { return RowBuf{base + (ph ? RowBuf::slots(N) : 0)}; }
+    };
+    __device__ __forceinline__ static Lds lds_of(cf* base) { return Lds{base, 0}; }
     // wide row groups: the partners through the LDS exchange buffer (every lane of the block takes part)
     template <bool INV>
-    __device__ __forceinline__ static void combine_lds(cf (&v)[EM], const RowBuf& buf, const cf* __restrict__ tw, int t) {
-        xsync<1>();
+    __device__ __forceinline__ static void combine_lds(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
+        const RowBuf buf = l.cur();
+        if (!G::PP) __syncthreads();  // one buffer: its previous readers are done
         if (t < Ls) {
 #pragma unroll
             for (int j = 0; j < Es; ++j) buf.at(t + Ls * j) = v[j];
         }
-        xsync<1>();
+        __syncthreads();
 #pragma unroll
         for (int j = 0; j < Es; ++j) {
             const int k = t + Ls * j;
@@ -235,8 +266,8 @@ template <int N> struct RowXfM {
                 v[j] = one<INV>(k, x, buf.at(kp >= 0 ? kp : 0), tw);
             }
         }
+        if (G::PP) l.ph ^= 1;
     }
-
     // The Hermitian combine of element k = t + Ls j with its partner N - k, which sits in lane
     // Ls - t, register Es - 1 - j (t = 0: this lane, register Es - j).  Registers j and Es - 1 - j are
     // each other's partner registers, so they are combined as a pair from one pair of shuffles (no
@@ -268,34 +299,50 @@ template <int N> struct RowXfM {
         }
     }
     // row spectrum in layout(Es) (v[j], j < Es) -> pixel pairs in layout(Ep) (v[j], j < Ep), x 2W
-    __device__ __forceinline__ static void c2r(cf (&v)[EM], const RowBuf& buf, const cf* __restrict__ tw, int t) {
-        if constexpr (WIDE) combine_lds<true>(v, buf, tw, t);
-        else combine<true>(v, tw, t);
-        mfft<N, Lg, EM, +1, SYNC, 2>(v, buf, tw, t, typename MRow<N>::Inv{});
+    __device__ __forceinline__ static void c2r(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
+        if constexpr (G::PP) {
+            combine_lds<true>(v, l, tw, t);
+            mfft_pp<N, Lg, EM, +1, 2>(v, l.base, RowBuf::slots(N), l.ph, tw, t, typename MRow<N>::Inv{});
+        } else if constexpr (WIDE) {
+            combine_lds<true>(v, l, tw, t);
+            mfft<N, Lg, EM, +1, 1, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Inv{});
+        } else {
+            combine<true>(v, tw, t);
+            mfft<N, Lg, EM, +1, 0, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Inv{});
+        }
     }
     // pixel pairs in layout(Ep) -> packed spectrum (2 rfft) in layout(Es)
-    __device__ __forceinline__ static void r2c(cf (&v)[EM], const RowBuf& buf, const cf* __restrict__ tw, int t) {
-        mfft<N, Lg, EM, -1, SYNC, 2>(v, buf, tw, t, typename MRow<N>::Fwd{});
-        if constexpr (WIDE) combine_lds<false>(v, buf, tw, t);
-        else combine<false>(v, tw, t);
+    __device__ __forceinline__ static void r2c(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
+        if constexpr (G::PP) {
+            mfft_pp<N, Lg, EM, -1, 2>(v, l.base, RowBuf::slots(N), l.ph, tw, t, typename MRow<N>::Fwd{});
+            combine_lds<false>(v, l, tw, t);
+        } else if constexpr (WIDE) {
+            mfft<N, Lg, EM, -1, 1, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Fwd{});
+            combine_lds<false>(v, l, tw, t);
+        } else {
+            mfft<N, Lg, EM, -1, 0, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Fwd{});
+            combine<false>(v, tw, t);
+        }
     }
     // the value of pixel-pair neighbour k + SHIFT (SHIFT = -1 / +1, circular) of every pair this lane
     // holds: lane shuffles within a wave, the LDS buffer across the waves of a wide row group
     template <int SHIFT>
-    __device__ __forceinline__ static void neighbour(const float (&val)[Ep], float (&out)[Ep], const RowBuf& buf, int t) {
+    __device__ __forceinline__ static void neighbour(const float (&val)[Ep], float (&out)[Ep], Lds& l, int t) {
         if constexpr (WIDE) {
-            xsync<1>();
+            const RowBuf buf = l.cur();
+            if (!G::PP) __syncthreads();
             if (t < Lp) {
 #pragma unroll
                 for (int j = 0; j < Ep; ++j) buf.at(t + Lp * j).x = val[j];
             }
-            xsync<1>();
+            __syncthreads();
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
                 int k = t + Lp * j + SHIFT;
                 k = k < 0 ? N - 1 : k >= N ? 0 : k;
                 out[j] = buf.at(k).x;
             }
+            if (G::PP) l.ph ^= 1;
         } else {
             const int src = SHIFT < 0 ? (t == 0 ? Lp - 1 : t - 1) : (t + 1 >= Lp ? 0 : t + 1);
             float sh[Ep];
@@ -325,14 +372,14 @@ __global__ void __launch_bounds__(256) k_row_r2c_m(const float* __restrict__ img
     const bool ok = row < rows;
     if (!G::WIDE && !ok) return;  // (a wide row group keeps every lane for the block barriers)
     if (!ok) row = rows - 1;
-    RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
+    auto lx = RowXfM<N>::lds_of(tw + G::W + sgl * G::NBUF * RowBuf::slots(N));
     const cf* src = reinterpret_cast<const cf*>(img + row * G::W);
     cf v[EM];
     if (t < Lp) {
 #pragma unroll
         for (int j = 0; j < Ep; ++j) v[j] = src[t + Lp * j];
     }
-    RowXfM<N>::r2c(v, buf, tw, t);
+    RowXfM<N>::r2c(v, lx, tw, t);
     if (ok && t < Ls) {
         cf* dst = spec + row * N;
 #pragma unroll
@@ -355,14 +402,14 @@ __global__ void __launch_bounds__(256) k_row_c2r_m(const cf* __restrict__ spec, 
     const bool ok = row < rows;
     if (!G::WIDE && !ok) return;
     if (!ok) row = rows - 1;
-    RowBuf buf{tw + G::W + sgl * RowBuf::slots(N)};
+    auto lx = RowXfM<N>::lds_of(tw + G::W + sgl * G::NBUF * RowBuf::slots(N));
     const cf* src = spec + row * N;
     cf v[EM];
     if (t < Ls) {
 #pragma unroll
         for (int j = 0; j < Es; ++j) v[j] = src[t + Ls * j];
     }
-    RowXfM<N>::c2r(v, buf, tw, t);
+    RowXfM<N>::c2r(v, lx, tw, t);
     if (ok && t < Lp) {
         cf* dst = reinterpret_cast<cf*>(img + row * G::W);
 #pragma unroll
@@ -482,7 +529,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
     const int spp = H / R;
     const long long p = strip / spp;
     const int i0 = (int)(strip % spp) * R;
-    RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    auto lx = RowXfM<N>::lds_of(tw + W + sgl * G::NBUF * RowBuf::slots(N));
     const float rho = a.rho[0];
     const float tau = a.lam[0] / rho;
     const bool pa = t < Lp, sa = t < Ls;  // lane holds pixels / spectrum elements
@@ -506,7 +553,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
 #pragma unroll
             for (int j = 0; j < Es; ++j) v[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + Ls * j]);
         }
-        RowXfM<N>::c2r(v, buf, tw, t);
+        RowXfM<N>::c2r(v, lx, tw, t);
 #pragma unroll
         for (int j = 0; j < Ep; ++j) x[j] = v[j];
     };
@@ -549,7 +596,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
             float wxs[Ep], wrs[Ep];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) wxs[j] = wxp[j].x;
-            RowXfM<N>::template neighbour<+1>(wxs, wrs, buf, t);  // w_x at pixel q1+1
+            RowXfM<N>::template neighbour<+1>(wxs, wrs, lx, t);  // w_x at pixel q1+1
             cf r[EM];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
@@ -559,7 +606,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
                 r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
             }
-            RowXfM<N>::r2c(r, buf, tw, t);
+            RowXfM<N>::r2c(r, lx, tw, t);
             if (sst) {
 #pragma unroll
                 for (int j = 0; j < Es; ++j) sta(&so[rm + t + Ls * j], r[j]);
@@ -576,7 +623,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
                 if constexpr (ISO) fx[j] = pa ? nsx[ro + t + Lp * j] : mkc(0.f, 0.f);
                 xys[j] = xcur[j].y;
             }
-            RowXfM<N>::template neighbour<-1>(xys, xls, buf, t);  // x at pixel q0-1
+            RowXfM<N>::template neighbour<-1>(xys, xls, lx, t);  // x at pixel q0-1
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
                 const float xl = xls[j];
@@ -621,7 +668,7 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
     const int g = (int)(item % H);
     const int grp = (int)(item / H);
     const int gm = g == 0 ? H - 1 : g - 1;
-    RowBuf buf{tw + W + sgl * RowBuf::slots(N)};
+    auto lx = RowXfM<N>::lds_of(tw + W + sgl * G::NBUF * RowBuf::slots(N));
     const bool pa = t < Lp, sa = t < Ls;
     cf sx[Ep], sy[Ep];
 #pragma unroll
@@ -637,15 +684,15 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
                 vc[j] = sp[(size_t)g * N + t + Ls * j];
             }
         }
-        RowXfM<N>::c2r(vp, buf, tw, t);
-        RowXfM<N>::c2r(vc, buf, tw, t);
+        RowXfM<N>::c2r(vp, lx, tw, t);
+        RowXfM<N>::c2r(vc, lx, tw, t);
         const size_t ro = (size_t)p * H * N + (size_t)g * N;  // cf units == pixel pairs
         const cf* uxi = reinterpret_cast<const cf*>(a.uxi);
         const cf* uyi = reinterpret_cast<const cf*>(a.uyi);
         float xys[Ep], xls[Ep];
 #pragma unroll
         for (int j = 0; j < Ep; ++j) xys[j] = vc[j].y;
-        RowXfM<N>::template neighbour<-1>(xys, xls, buf, t);
+        RowXfM<N>::template neighbour<-1>(xys, xls, lx, t);
 #pragma unroll
         for (int j = 0; j < Ep; ++j) {
             const cf ux = (FIRST || !pa) ? mkc(0.f, 0.f) : uxi[ro + t + Lp * j];
