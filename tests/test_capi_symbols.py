@@ -57,7 +57,8 @@ def test_host_entry_points():
     assert [lib.admm_tv_supported(*hw) for hw in ((65537, 16), (16, 70000), (0, 16))] == [0] * 3
     # smooth sizes with transform plans: the fused iteration on mixed-radix transforms (inference)
     assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1920), (720, 1280), (480, 640), (2160, 512), (2160, 3840),
-                                                  (1024, 4096), (4096, 4096))] == [3] * 7
+                                                  (1024, 4096), (4096, 4096), (600, 800), (1200, 1600), (1440, 2560),
+                                                  (1536, 2048))] == [3] * 11
     assert [lib.admm_tv_supported(*hw) for hw in ((1080, 7680), (1081, 1920), (1080, 1918))] == [generic] * 3
     d = _native.desc(64, 3, 1024, 1024, 21, False, 50)
     ws = _native.workspace_size(d)

@@ -35,7 +35,9 @@ def test_supported_codes():
     from admmtor import _native
     lib = _native.load()
     assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1920), (720, 1280), (480, 640), (2160, 1024), (1024, 960),
-                                                  (540, 1080), (360, 720), (240, 480), (2160, 3840), (4096, 4096))] == [3] * 10
+                                                  (540, 1080), (360, 720), (240, 480), (2160, 3840), (4096, 4096),
+                                                  (600, 800), (768, 1024), (1200, 1600), (1536, 2048), (1080, 1440),
+                                                  (1440, 2560), (800, 800))] == [3] * 17
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (4096, 2048))] == [1] * 2
     assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1921), (1080, 7680), (1000, 1920), (481, 321))] == [2] * 4
 
@@ -56,6 +58,13 @@ CASES = [
     ((1, 1, 2160, 3840), ("gauss:2", 11), False, 5),     # 4K UHD: 4-wave row groups (1920 = 8*15*16), 2160 columns
     ((1, 1, 4096, 4096), ("gauss:1.5", 9), True, 4),     # 4096-wide power-of-two rows: 4-wave groups (8*4*8*8)
     ((1, 2, 1080, 2048), None, False, 6),                # 2048-wide rows as 2-wave groups beside 1080 columns
+    ((2, 2, 600, 800), ("motion", 9), False, 10),        # SVGA: rows 400 = 10*5*8, cols 6*10*10
+    ((1, 2, 768, 1024), ("gauss:1.5", 9), True, 8),      # XGA: power-of-two rows, 768-point columns (6*2*8*8)
+    ((1, 1, 1200, 1600), ("gauss:2", 11), False, 6),     # UXGA: 4-wave row groups, 5 pixel pairs per lane
+    ((1, 1, 1536, 2048), None, False, 4),                # QXGA: 1536-point columns, 4 per block
+    ((1, 1, 1080, 1440), ("random", 5), True, 5),        # rows 720 = 12*10*6 over 120 of 128 lanes
+    ((1, 1, 1440, 2560), ("gauss:1.5", 9), False, 4),    # QHD: rows 1280 = 8*4*8*5, cols 12*8*15
+    ((1, 1, 800, 800), ("motion", 7), True, 6),          # 800-point columns beside 400-point rows
 ]
 
 

@@ -30,6 +30,10 @@ template <class F> hipError_t with_row(int N, F&& f) {
         case 960: return f(std::integral_constant<int, 960>{});
         case 1920: return f(std::integral_constant<int, 1920>{});
         case 2048: return f(std::integral_constant<int, 2048>{});
+        case 400: return f(std::integral_constant<int, 400>{});
+        case 720: return f(std::integral_constant<int, 720>{});
+        case 800: return f(std::integral_constant<int, 800>{});
+        case 1280: return f(std::integral_constant<int, 1280>{});
         default: return hipErrorInvalidValue;
     }
 }
@@ -53,6 +57,12 @@ template <class F> hipError_t with_col(int H, F&& f) {
         case 960: return f(std::integral_constant<int, 960>{});
         case 1080: return f(std::integral_constant<int, 1080>{});
         case 2160: return f(std::integral_constant<int, 2160>{});
+        case 600: return f(std::integral_constant<int, 600>{});
+        case 768: return f(std::integral_constant<int, 768>{});
+        case 800: return f(std::integral_constant<int, 800>{});
+        case 1200: return f(std::integral_constant<int, 1200>{});
+        case 1440: return f(std::integral_constant<int, 1440>{});
+        case 1536: return f(std::integral_constant<int, 1536>{});
         default: return hipErrorInvalidValue;
     }
 }

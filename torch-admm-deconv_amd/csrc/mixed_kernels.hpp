@@ -110,6 +110,27 @@ template <> struct MRow<540> {  // W = 1080: spectra 45 x 12, pixels 60 x 9
     using Inv = Sched<12, 5, 9>;
     using Fwd = Sched<9, 5, 12>;
 };
+// common photo / display widths (plans from tools/mixed_plans.py, each simulated to ~1e-15)
+template <> struct MRow<400> {  // W = 800 (SVGA): spectra 40 x 10, pixels 50 x 8
+    static constexpr int Lg = 64, Lp = 50, Ep = 8, Ls = 40, Es = 10;
+    using Inv = Sched<10, 5, 8>;
+    using Fwd = Sched<8, 5, 10>;
+};
+template <> struct MRow<720> {  // W = 1440: spectra 60 x 12, pixels 120 x 6 (2 waves)
+    static constexpr int Lg = 128, Lp = 120, Ep = 6, Ls = 60, Es = 12;
+    using Inv = Sched<12, 10, 6>;
+    using Fwd = Sched<6, 10, 12>;
+};
+template <> struct MRow<800> {  // W = 1600: spectra 100 x 8, pixels 160 x 5 (4 waves)
+    static constexpr int Lg = 256, Lp = 160, Ep = 5, Ls = 100, Es = 8;
+    using Inv = Sched<8, 4, 5, 5>;
+    using Fwd = Sched<5, 5, 4, 8>;
+};
+template <> struct MRow<1280> {  // W = 2560: spectra 160 x 8, pixels 256 x 5 (4 waves)
+    static constexpr int Lg = 256, Lp = 256, Ep = 5, Ls = 160, Es = 8;
+    using Inv = Sched<8, 4, 8, 5>;
+    using Fwd = Sched<5, 8, 4, 8>;
+};
 
 #ifndef ADMM_MIXED_PP
 #define ADMM_MIXED_PP 0
@@ -196,6 +217,37 @@ template <> struct MCol<240> {
     static constexpr int Lc = 16, Ec = 15, C = 8;
     using Fwd = Sched<15, 16>;
     using Inv = Sched<16, 15>;
+};
+// common photo / display heights (tools/mixed_plans.py)
+template <> struct MCol<600> {
+    static constexpr int Lc = 100, Ec = 6, C = 8;
+    using Fwd = Sched<6, 10, 10>;
+    using Inv = Sched<10, 10, 6>;
+};
+template <> struct MCol<768> {
+    static constexpr int Lc = 128, Ec = 6, C = 8;
+    using Fwd = Sched<6, 2, 8, 8>;
+    using Inv = Sched<8, 8, 2, 6>;
+};
+template <> struct MCol<800> {
+    static constexpr int Lc = 100, Ec = 8, C = 8;
+    using Fwd = Sched<8, 10, 10>;
+    using Inv = Sched<10, 10, 8>;
+};
+template <> struct MCol<1200> {
+    static constexpr int Lc = 120, Ec = 10, C = 8;
+    using Fwd = Sched<10, 10, 12>;
+    using Inv = Sched<12, 10, 10>;
+};
+template <> struct MCol<1440> {
+    static constexpr int Lc = 120, Ec = 12, C = 8;
+    using Fwd = Sched<12, 8, 15>;
+    using Inv = Sched<15, 8, 12>;
+};
+template <> struct MCol<1536> {
+    static constexpr int Lc = 256, Ec = 6, C = 4;
+    using Fwd = Sched<6, 4, 8, 8>;
+    using Inv = Sched<8, 8, 4, 6>;
 };
 
 template <int H> struct MColG {
