@@ -157,6 +157,10 @@ struct Layout {
     size_t gscr;  // generic path, lines beyond the LDS image: the transform blocks' scratch slots
     int ngroups, ppg;
     bool gen;
+    // generic fp32 inference with both matrix-core plans: the half-spectrum row pitch (complex values)
+    // padded to a multiple of 16 (128 B), so the column pass's 16-column row segments are whole cache
+    // lines (A/B knob ADMM_GEN_PITCH=0: Wh)
+    int ldw;
 };
 
 Layout make_layout(const admm_tv_desc& d) {
@@ -180,7 +184,9 @@ Layout make_layout(const admm_tv_desc& d) {
         L.mmr = mm_plan_row((int)W);
     }
     L.mixed = L.gen && !f64 && G == 1 && mixed_hw(d.H, d.W);
-    L.spec[0] = take(L.gen ? P * H * (N + 1) * csz : img);
+    L.ldw = (int)(N + 1);
+    if (L.gen && !f64 && L.mm.ok && L.mmr.ok && env_int("ADMM_GEN_PITCH", 1)) L.ldw = (int)((N + 1 + 15) / 16 * 16);
+    L.spec[0] = take(L.gen ? P * H * (size_t)L.ldw * csz : img);
     L.spec[1] = take(img);
     L.rimg = L.gen ? take(img) : 0;
     for (int i = 0; i < 4; ++i) L.u[i] = take(img);
@@ -1061,10 +1067,10 @@ inline dim3 gen_grid(long long items, const GPlan& p, size_t csz) {
     if ((pl).glb && !(gscr)) return fail(ADMM_TV_EINVAL, "long lines: no scratch region");
 template <class T>
 int grow_fwd(const T* img, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, hipStream_t s,
-             cx_t<T>* gscr = nullptr) {
+             cx_t<T>* gscr = nullptr, int ldw = 0) {
     const GPlan pl = make_plan(W, kF64<T>);
     GLB_CHECK(pl, gscr)
-    GRowArgsT<T> a{img, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr};
+    GRowArgsT<T> a{img, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr, ldw};
     const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
     return with_plan_t<T>(a.plan, [&](auto bm, auto twg, auto glb) {
         constexpr int BM = decltype(bm)::value;
@@ -1086,10 +1092,10 @@ int grow_fwd(const T* img, cx_t<T>* spec, const cx_t<T>* tw, int W, long long ro
 // the step fused into the row transform of r (k_grow_fwd_step; inference iterations)
 template <bool ISO, bool FIRST, class T>
 int grow_fwd_step_t(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, hipStream_t s,
-                    cx_t<T>* gscr) {
+                    cx_t<T>* gscr, int ldw) {
     const GPlan pl = make_plan(W, kF64<T>);
     GLB_CHECK(pl, gscr)
-    GRowArgsT<T> a{nullptr, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr};
+    GRowArgsT<T> a{nullptr, spec, nullptr, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr, ldw};
     const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
     return with_plan_t<T>(a.plan, [&](auto bm, auto twg, auto glb) {
         constexpr int BM = decltype(bm)::value;
@@ -1110,11 +1116,11 @@ int grow_fwd_step_t(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, in
 }
 template <class T>
 int grow_fwd_step(const GStepArgsT<T>& g, cx_t<T>* spec, const cx_t<T>* tw, int W, long long rows, bool iso,
-                  bool first, hipStream_t s, cx_t<T>* gscr = nullptr) {
-    if (iso) return first ? grow_fwd_step_t<true, true>(g, spec, tw, W, rows, s, gscr)
-                          : grow_fwd_step_t<true, false>(g, spec, tw, W, rows, s, gscr);
-    return first ? grow_fwd_step_t<false, true>(g, spec, tw, W, rows, s, gscr)
-                 : grow_fwd_step_t<false, false>(g, spec, tw, W, rows, s, gscr);
+                  bool first, hipStream_t s, cx_t<T>* gscr = nullptr, int ldw = 0) {
+    if (iso) return first ? grow_fwd_step_t<true, true>(g, spec, tw, W, rows, s, gscr, ldw)
+                          : grow_fwd_step_t<true, false>(g, spec, tw, W, rows, s, gscr, ldw);
+    return first ? grow_fwd_step_t<false, true>(g, spec, tw, W, rows, s, gscr, ldw)
+                 : grow_fwd_step_t<false, false>(g, spec, tw, W, rows, s, gscr, ldw);
 }
 template <int S> int grow_inv_mm_launch(const GRowInvMMArgs& a, size_t lds, int nth, hipStream_t s) {
     const dim3 grid((unsigned)((a.rows + 2 * a.NL - 1) / (2 * a.NL)));
@@ -1130,12 +1136,13 @@ template <int S> int grow_inv_mm_launch(const GRowInvMMArgs& a, size_t lds, int 
 // mmr: the layout's row-inverse plan (Layout::mmr)
 template <class T>
 int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long rows, hipStream_t s,
-             cx_t<T>* gscr, const MMPlan& mmr) {
+             cx_t<T>* gscr, const MMPlan& mmr, int ldw = 0) {
     if constexpr (!kF64<T>) {
         const MMPlan m = mmr;
         if (m.ok && rows > 0) {
             const int Wh = W / 2 + 1;
-            GRowInvMMArgs a{spec, img, tw, rows, W, m.R, m.h, m.KS, m.MT, m.NL, m.RP, Wh, 2 * m.NL * Wh * 2};
+            GRowInvMMArgs a{spec, img, tw, rows, W, m.R, m.h, m.KS, m.MT, m.NL, m.RP, Wh, 2 * m.NL * Wh * 2,
+                            ldw ? ldw : Wh};
             switch (m.S) {
                 case 1: return grow_inv_mm_launch<1>(a, m.lds, m.nth, s);
                 case 2: return grow_inv_mm_launch<2>(a, m.lds, m.nth, s);
@@ -1149,7 +1156,7 @@ int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long ro
     }
     const GPlan pl = make_plan(W, kF64<T>);
     GLB_CHECK(pl, gscr)
-    GRowArgsT<T> a{nullptr, const_cast<cx_t<T>*>(spec), img, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr};
+    GRowArgsT<T> a{nullptr, const_cast<cx_t<T>*>(spec), img, tw, pl, rows, grow_lines(W, pl, kCsz<T>), gscr, ldw};
     const size_t lds = glds(W, a.lines, a.plan, kCsz<T>);
     return with_plan_t<T>(a.plan, [&](auto bm, auto twg, auto glb) {
         constexpr int BM = decltype(bm)::value;
@@ -1208,13 +1215,13 @@ inline int mm_dbg() { return ADMM_MM_DBG_BUILD ? env_int("ADMM_MM_DBG", 0) : 0; 
 // mm: the layout's column-pass plan (Layout::mm; its factor copy was sized and written for it)
 template <class T>
 int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx_t<T>* tw, int H, int W, long long P,
-         int mode, hipStream_t s, cx_t<T>* gscr, const MMPlan& mm) {
+         int mode, hipStream_t s, cx_t<T>* gscr, const MMPlan& mm, int ldw = 0) {
     if constexpr (!kF64<T>) {
         const MMPlan m = mm;
         if (mode == 0 && m.ok) {  // the factor's [H][Wh] copy follows fcT (setup, k_fc_transpose)
             const int Wh = W / 2 + 1;
             GColMMArgs a{spec, dump, fcT + (size_t)Wh * H, tw, H, m.R, m.h, m.KS, m.MT, m.NL, __builtin_ctz(m.NL), m.RP,
-                         Wh, (Wh + m.NL - 1) / m.NL, P, mm_dbg()};
+                         Wh, (Wh + m.NL - 1) / m.NL, P, mm_dbg(), ldw ? ldw : Wh};
             switch (m.S) {
                 case 1: return gcol_mm_launch<1>(a, m.lds, s);
                 case 2: return gcol_mm_launch<2>(a, m.lds, s);
@@ -1229,6 +1236,7 @@ int gcol(cx_t<T>* spec, cx_t<T>* dump, const T* fcT, const cx_t<T>* mT, const cx
     const GPlan pl = make_plan(H, kF64<T>);
     GLB_CHECK(pl, gscr)
     const int Wh = W / 2 + 1, cols = gcol_cols(H, pl, kCsz<T>);
+    if (ldw && ldw != Wh) return fail(ADMM_TV_EINVAL, "padded spectrum pitch without the matrix-core column pass");
     const int colblocks = (Wh + cols - 1) / cols;
     GColArgsT<T> a{spec, dump, fcT, mT, tw, pl, Wh, cols, colblocks, P, gscr};
     const size_t lds = glds(H, cols, a.plan, kCsz<T>);
@@ -1360,7 +1368,9 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     // the iteration loop over planes [p0, p0 + np) on stream st (every plane, or -- aniso inference,
     // whose planes are independent -- one half per stream, ADMM_GEN_STREAMS)
     auto solve_planes = [&](long long p0, long long np, hipStream_t st) -> int {
-    const size_t so = (size_t)p0 * H * (W / 2 + 1), io = (size_t)p0 * H * W;  // cf / float offsets
+    // the inference iteration's spectrum pitch (Layout::ldw); training keeps Wh (its history layout)
+    const int ld = train ? W / 2 + 1 : Lo.ldw;
+    const size_t so = (size_t)p0 * H * ld, io = (size_t)p0 * H * W;  // cf / float offsets
     C* cspec = spec + so;
     T* cx = ximg + io;
     T* crimg = rimg + io;
@@ -1369,15 +1379,15 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     const long long crows = np * H;
     {
         ProfScope ps(3, st);
-        if (int e = grow_fwd(cb, cspec, twW, W, crows, st, gs)) return e;  // r_1 = b
+        if (int e = grow_fwd(cb, cspec, twW, W, crows, st, gs, ld)) return e;  // r_1 = b
     }
     int uin = 0;
     for (int it = 1; it <= d.maxit; ++it) {
         const bool last = it == d.maxit;
         {
             ProfScope ps(1, st);
-            if (int e = gcol<T>(cspec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, np, 0, st, gs, Lo.mm)) return e;
-            if (int e = grow_inv<T>(cspec, last ? cout : cx, twW, W, crows, st, gs, Lo.mmr)) return e;
+            if (int e = gcol<T>(cspec, keep_t ? ht(it) : nullptr, fcT, mT, twH, H, W, np, 0, st, gs, Lo.mm, ld)) return e;
+            if (int e = grow_inv<T>(cspec, last ? cout : cx, twW, W, crows, st, gs, Lo.mmr, ld)) return e;
         }
         if (last && !train) break;
         const T* xk = last ? cout : cx;
@@ -1417,11 +1427,11 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
             GStepArgsT<T> ga{xk, cb, uxi, uyi, uxo, uyo, last ? nullptr : crimg, nsq, nprev, lam, rho, H, W, np * H * W};
             // inference: the step runs inside the row transform of r (ADMM_GSTEP_FUSE=0: separate)
             if (!train && !last && env_int("ADMM_GSTEP_FUSE", 1)) {
-                if (int e = grow_fwd_step(ga, cspec, twW, W, crows, d.iso != 0, first, st, gs)) return e;
+                if (int e = grow_fwd_step(ga, cspec, twW, W, crows, d.iso != 0, first, st, gs, ld)) return e;
             } else {
                 if (int e = gstep(ga, d.iso != 0, first, train, st)) return e;
                 if (!last)
-                    if (int e = grow_fwd(crimg, cspec, twW, W, crows, st, gs)) return e;
+                    if (int e = grow_fwd(crimg, cspec, twW, W, crows, st, gs, ld)) return e;
             }
         }
         uin = 1 - uin;

@@ -40,6 +40,7 @@ struct GColMMArgs {
     int H, R, h, KS, MT, NL, lgNL, RP, Wh, colblocks;
     long long P;
     int dbg;  // timing experiments only (ADMM_MM_DBG): phases to skip, results invalid when set
+    int ldw;  // spectrum row pitch in complex values (>= Wh; the factor and the dump keep Wh)
 };
 
 typedef float mm_f32x4 __attribute__((ext_vector_type(4)));
@@ -157,7 +158,8 @@ k_gcol_mm(GColMMArgs a) {
     const long long item = blockIdx.x;
     const long long p = item / a.colblocks;
     const int c0 = (int)(item % a.colblocks) * NL;
-    cf* Sp = a.spec + (size_t)p * H * Wh + c0;
+    const int ld = a.ldw;
+    cf* Sp = a.spec + (size_t)p * H * ld + c0;
     cf* Dp = a.dump ? a.dump + (size_t)p * H * Wh : nullptr;  // indexed by the absolute column kx
     cf* twl = reinterpret_cast<cf*>(F + 4 * KS * RP);       // the H twiddles, after the image
 
@@ -180,8 +182,8 @@ k_gcol_mm(GColMMArgs a) {
             const int n2 = rest % S, q = rest / S;
             x0[u] = x1[u] = mkc(0.f, 0.f);
             if (!(a.dbg & 8) && it < nload && c0 + L < Wh) {
-                x0[u] = Sp[(size_t)(n2 + S * q) * Wh + L];
-                if (q) x1[u] = Sp[(size_t)(n2 + S * (R - q)) * Wh + L];
+                x0[u] = Sp[(size_t)(n2 + S * q) * ld + L];
+                if (q) x1[u] = Sp[(size_t)(n2 + S * (R - q)) * ld + L];
             }
         });
         static_for<0, kMMU>([&](auto uc) {
@@ -285,8 +287,8 @@ k_gcol_mm(GColMMArgs a) {
         const int n2 = rest % S, n1 = rest / S;
         if (c0 + L >= Wh || (a.dbg & 16)) continue;
         const float4 v = *reinterpret_cast<const float4*>(&F[n1 * RP + 4 * (n2 * NL + L)]);
-        Sp[(size_t)(n2 + S * n1) * Wh + L] = mkc(v.x, v.z);
-        if (n1) Sp[(size_t)(n2 + S * (R - n1)) * Wh + L] = mkc(v.y, v.w);
+        Sp[(size_t)(n2 + S * n1) * ld + L] = mkc(v.x, v.z);
+        if (n1) Sp[(size_t)(n2 + S * (R - n1)) * ld + L] = mkc(v.y, v.w);
     }
 }
 
@@ -309,6 +311,7 @@ struct GRowInvMMArgs {
     long long rows;
     int W, R, h, KS, MT, NL, RP, Wh;
     int stage;       // floats of the staged spectrum rows (the image region starts at 0 too)
+    int ldw;         // spectrum row pitch in complex values (>= Wh)
 };
 
 template <int S, int NTH = 256>
@@ -331,10 +334,15 @@ k_grow_inv_mm(GRowInvMMArgs a) {
     const int mt = wv % MT, tile0 = wv / MT, tstep = G;
     const int ntw = gw ? (NT - tile0 + G - 1) / G : 0;
 
-    {   // stage: the block's rows are contiguous in the spectrum
-        const cf* src = a.spec + r0 * Wh;
-        const int n = nrows * Wh;
-        for (int i = tid; i < n; i += NTH) Xs[i] = src[i];
+    {   // stage: the block's rows (contiguous in the spectrum when the pitch is Wh)
+        const cf* src = a.spec + r0 * a.ldw;
+        if (a.ldw == Wh) {
+            const int n = nrows * Wh;
+            for (int i = tid; i < n; i += NTH) Xs[i] = src[i];
+        } else {
+            for (int r = 0; r < nrows; ++r)
+                for (int i = tid; i < Wh; i += NTH) Xs[r * Wh + i] = src[(size_t)r * a.ldw + i];
+        }
         for (int i = nrows * Wh + tid; i < 2 * NL * Wh; i += NTH) Xs[i] = mkc(0.f, 0.f);
         for (int i = tid; i < W; i += NTH) twl[i] = a.tw[i];
     }

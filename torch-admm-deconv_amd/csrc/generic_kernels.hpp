@@ -459,6 +459,7 @@ template <class T> struct GRowArgsT {
     long long rows;
     int lines;           // rows per block
     cx_t<T>* gscr;       // plan.glb: the blocks' scratch slots, 2 W lines values each
+    int ldw;             // spectrum row pitch in complex values (0: Wh = W / 2 + 1)
 };
 
 // the line buffers of a transform block: the LDS image after the twiddles (twl), or -- long lines
@@ -491,13 +492,14 @@ __device__ __forceinline__ void grow_fwd_item(const GRowArgsT<T>& a, cx_t<T>* A,
     __syncthreads();
     const C* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
     const T half = T(0.5);
+    const long long ld = a.ldw ? a.ldw : Wh;
     for (int c = 0; c < lines; ++c)
         for (int k = threadIdx.x; k < Wh; k += blockDim.x) {
             const C z = res[k * lines + c];
             const C m = res[(k == 0 ? 0 : W - k) * lines + c];
             const long long ra = r0 + 2 * c;
-            if (2 * c < nl) a.spec[ra * Wh + k] = mkx<T>(half * (z.x + m.x), half * (z.y - m.y));
-            if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkx<T>(half * (z.y + m.y), half * (m.x - z.x));
+            if (2 * c < nl) a.spec[ra * ld + k] = mkx<T>(half * (z.x + m.x), half * (z.y - m.y));
+            if (2 * c + 1 < nl) a.spec[(ra + 1) * ld + k] = mkx<T>(half * (z.y + m.y), half * (m.x - z.x));
         }
 }
 
@@ -537,13 +539,14 @@ __device__ __forceinline__ void grow_inv_item(const GRowArgsT<T>& a, cx_t<T>* A,
     const int nl = (int)min((long long)2 * lines, a.rows - r0);
     // Hermitian completion of a half spectrum: X[k] = conj X[W - k] for k >= Wh; the imaginary
     // parts of the self-conjugate bins (DC, and Nyquist for even W) are dropped, as irfft does
+    const long long ld = a.ldw ? a.ldw : Wh;
     auto full = [&](long long row, int k) -> C {
         if (k < Wh) {
-            C v = a.spec[row * Wh + k];
+            C v = a.spec[row * ld + k];
             if (k == 0 || 2 * k == W) v.y = T(0);
             return v;
         }
-        return cconj(a.spec[row * Wh + (W - k)]);
+        return cconj(a.spec[row * ld + (W - k)]);
     };
     for (int c = 0; c < lines; ++c)
         for (int k = threadIdx.x; k < W; k += blockDim.x) {
@@ -789,13 +792,14 @@ __device__ __forceinline__ void grow_fwd_step_item(const GRowArgsT<T>& a, const 
     __syncthreads();
     const C* res = gfft_lds<-1, BM>(A, B, a.plan, lines, tw, X);
     const T half = T(0.5);
+    const long long ld = a.ldw ? a.ldw : Wh;
     for (int c = 0; c < lines; ++c)
         for (int k = threadIdx.x; k < Wh; k += blockDim.x) {
             const C z = res[k * lines + c];
             const C m = res[(k == 0 ? 0 : W - k) * lines + c];
             const long long ra = r0 + 2 * c;
-            if (2 * c < nl) a.spec[ra * Wh + k] = mkx<T>(half * (z.x + m.x), half * (z.y - m.y));
-            if (2 * c + 1 < nl) a.spec[(ra + 1) * Wh + k] = mkx<T>(half * (z.y + m.y), half * (m.x - z.x));
+            if (2 * c < nl) a.spec[ra * ld + k] = mkx<T>(half * (z.x + m.x), half * (z.y - m.y));
+            if (2 * c + 1 < nl) a.spec[(ra + 1) * ld + k] = mkx<T>(half * (z.y + m.y), half * (m.x - z.x));
         }
 }
 
