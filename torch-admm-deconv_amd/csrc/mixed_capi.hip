@@ -1,6 +1,7 @@
 // mixed_capi.hip -- launchers of the mixed-radix fused kernels (mixed_kernels.hpp):
 // the plan tables dispatched to their template instances.  The solve itself is orchestrated in
 // admm_capi.hip (run_forward_mixed).
+#include <cstdlib>
 #include <type_traits>
 
 #include "mixed_capi.hpp"
@@ -92,9 +93,11 @@ int row_lanes(int N) {
     return l;
 }
 int col_cols(int H) {
+    // the fewest columns a block may take: pass_b launches the plan's C, or 4 or 2 when N = W / 2 is no
+    // multiple of it
     int c = 0;
     (void)with_col(H, [&](auto h) {
-        c = MColG<decltype(h)::value>::C;
+        c = MColG<decltype(h)::value>::C < 2 ? MColG<decltype(h)::value>::C : 2;
         return hipSuccess;
     });
     return c;
@@ -154,14 +157,33 @@ hipError_t iso_norm(int N, const IsoArgs& a, bool first, hipStream_t s) {
 hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s) {
     return with_col(H, [&](auto h) {
         constexpr int HH = decltype(h)::value;
-        using G = MColG<HH>;
-        const int colblocks = N / G::C;
-        // plane groups of two at H >= 1024 (k_pass_b's measured tile order), plane-major below
-        const int order = HH >= 1024 ? 2 : 1;
-        if (hipError_t e = lds(k_pass_b_m<HH>, G::lds_bytes())) return e;
-        hipLaunchKernelGGL(k_pass_b_m<HH>, dim3((unsigned)(P * colblocks)), dim3(G::NT), G::lds_bytes(), s, spec, fcM, twH,
-                           N, colblocks, order);
-        return hipGetLastError();
+        // plane groups of two at H >= 1024 (k_pass_b's measured tile order), plane-major below; A/B knob
+        // ADMM_PASSB_M_ORDER (read once per process: it changes no sizes)
+        static const int forced = [] {
+            const char* e = std::getenv("ADMM_PASSB_M_ORDER");
+            return e ? std::atoi(e) : 0;
+        }();
+        const int order = forced > 0 ? forced : (HH >= 1024 ? 2 : 1);
+        auto go = [&](auto cc) {
+            constexpr int CC = decltype(cc)::value;
+            using G = MColG<HH, CC>;
+            const int colblocks = N / CC;
+            if (hipError_t e = lds(k_pass_b_m<HH, CC>, G::lds_bytes())) return e;
+            hipLaunchKernelGGL((k_pass_b_m<HH, CC>), dim3((unsigned)(P * colblocks)), dim3(G::NT), G::lds_bytes(), s,
+                               spec, fcM, twH, N, colblocks, order);
+            return hipGetLastError();
+        };
+        // the plan's columns per block, or fewer when N is no multiple of them (e.g. W = 1080 beside the
+        // 8-column plans)
+        constexpr int C0 = MCol<HH>::C;
+        if (N % C0 == 0) return go(std::integral_constant<int, C0>{});
+        if constexpr (C0 > 4) {
+            if (N % 4 == 0) return go(std::integral_constant<int, 4>{});
+        }
+        if constexpr (C0 > 2) {
+            if (N % 2 == 0) return go(std::integral_constant<int, 2>{});
+        }
+        return hipErrorInvalidValue;
     });
 }
 

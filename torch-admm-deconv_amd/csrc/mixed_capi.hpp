@@ -13,7 +13,7 @@ using admm::cf;
 // plans exist for the row length N = W/2 / the column length H
 bool row_ok(int N);
 bool col_ok(int H);
-int col_cols(int H);  // columns per column-pass block (N must be a multiple)
+int col_cols(int H);  // the fewest columns per column-pass block (N must be a multiple)
 int row_lanes(int N);  // lanes of a row group (up to 256: several waves)
 
 hipError_t r2c(int N, const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s);

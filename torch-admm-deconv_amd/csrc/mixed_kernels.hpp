@@ -61,10 +61,17 @@ template <> struct MRow<1024> {  // W = 2048 beside a smooth H: 128 lanes x 8 (2
 #define ADMM_M960_V 0
 #endif
 template <> struct MRow<960> {  // W = 1920 (HD): 960 = 8 * 15 * 8 over 120 of 128 lanes
+#if ADMM_M960_V == 2  // 4-wave row groups, 4 pixel pairs per lane: 4 * 15 * 4 * 4 over 240 of 256 lanes
+    static constexpr int Lg = 256, Lp = 240, Ep = 4, Ls = 240, Es = 4;
+    using Inv = Sched<4, 15, 4, 4>;
+    using Fwd = Sched<4, 4, 15, 4>;
+#else
     static constexpr int Lg = 128, Lp = 120, Ep = 8, Ls = 120, Es = 8;
+#endif
 #if ADMM_M960_V == 1
     using Inv = Sched<8, 3, 5, 8>;
     using Fwd = Sched<8, 5, 3, 8>;
+#elif ADMM_M960_V == 2
 #else
     using Inv = Sched<8, 15, 8>;
     using Fwd = Sched<8, 15, 8>;
@@ -178,8 +185,17 @@ template <> struct MCol<4096> : MColPow2<4096> {};
 #ifndef ADMM_MCOL_C
 #define ADMM_MCOL_C 8
 #endif
+// ADMM_M1080_V (A/B build knob): 0 = 120 threads x 9 values per column (960-thread blocks: one block per
+// CU at 112 VGPRs), 1 = 60 threads x 18 values (480-thread blocks: two per CU, twice the bytes in flight)
+#ifndef ADMM_M1080_V
+#define ADMM_M1080_V 0
+#endif
 template <> struct MCol<1080> {
+#if ADMM_M1080_V == 1
+    static constexpr int Lc = 60, Ec = 18, C = ADMM_MCOL_C;
+#else
     static constexpr int Lc = 120, Ec = 9, C = ADMM_MCOL_C;
+#endif
     using Fwd = Sched<9, 15, 8>;
     using Inv = Sched<8, 15, 9>;
 };
@@ -250,9 +266,11 @@ template <> struct MCol<1536> {
     using Inv = Sched<8, 8, 4, 6>;
 };
 
-template <int H> struct MColG {
+// CC: columns per block of this instance -- the plan's C, or fewer when the row spectrum's N = W / 2
+// columns are not a multiple of it (mixed_capi.hip pass_b: C, 4 or 2)
+template <int H, int CC = MCol<H>::C> struct MColG {
     using P = MCol<H>;
-    static constexpr int Lc = P::Lc, Ec = P::Ec, C = P::C, NT = C * Lc;
+    static constexpr int Lc = P::Lc, Ec = P::Ec, C = CC, NT = C * Lc;
     static constexpr int Rz = sched_last(typename P::Fwd{});
     static constexpr int NBz = H / Rz, Qz = (NBz + Lc - 1) / Lc;
     static constexpr int a = sched_regs<H, Lc>(typename P::Fwd{}), b = sched_regs<H, Lc>(typename P::Inv{});
@@ -483,11 +501,18 @@ static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restri
 // ---------------------------------------------------------------------------------------------
 // pass B: column FFT -> Wiener factor -> column IFFT, in place, C columns per block
 // ---------------------------------------------------------------------------------------------
-template <int H>
-__global__ void __launch_bounds__(MColG<H>::NT) k_pass_b_m(cf* spec, const float* __restrict__ fcM,
+// ADMM_PASSB_M_WPE (A/B build knob): an occupancy target (waves per SIMD) for the smooth column plans, so
+// more blocks fit per CU (0: the compiler's choice)
+#ifndef ADMM_PASSB_M_WPE
+#define ADMM_PASSB_M_WPE 0
+#endif
+template <int H> constexpr int passb_m_wpe() { return (H & (H - 1)) == 0 ? 0 : ADMM_PASSB_M_WPE; }
+template <int H, int CC>
+__global__ void __launch_bounds__((MColG<H, CC>::NT)) __attribute__((amdgpu_waves_per_eu(passb_m_wpe<H>(), 0)))
+k_pass_b_m(cf* spec, const float* __restrict__ fcM,
                                                            const cf* __restrict__ twH_g, int N, int colblocks,
                                                            int order) {
-    using G = MColG<H>;
+    using G = MColG<H, CC>;
     constexpr int Lc = G::Lc, Ec = G::Ec, C = G::C, EM = G::EM, NBz = G::NBz, Qz = G::Qz;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
@@ -560,7 +585,11 @@ __global__ void __launch_bounds__(MColG<H>::NT) k_pass_b_m(cf* spec, const float
 // occupancy target of the mixed row pass (waves per SIMD): the plans keep <= 9 pixel pairs per lane
 // (wide row groups where a wave would need more), ~150-170 VGPRs: 2 guaranteed, 3 when they fit
 #ifndef PASSA_M_MINW
+#ifdef ADMM_PASSA_M_W  // A/B build knob: one occupancy target for every row plan
+#define PASSA_M_MINW(ep) (ADMM_PASSA_M_W)
+#else
 #define PASSA_M_MINW(ep) ((ep) > 9 ? 1 : 2)
+#endif
 #endif
 template <int N, bool ISO, bool FIRST>
 __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(PassAArgs a) {
