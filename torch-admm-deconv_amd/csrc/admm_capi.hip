@@ -1583,12 +1583,35 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
 
 // rows per strip of the mixed row pass: a divisor of H (8, 4, 2 or 1), halved while there are fewer than
 // ~2 waves per SIMD of strips (the row group of a plan is Lg lanes: 16 ... 256)
-int strip_rows_mixed(int H, long long rows, int lanes) {
-    int R = 8;
-    while (R > 1 && H % R) R /= 2;
-    const long long want = 2LL * 1024 * 64 / std::max(lanes, 1);
-    while (R > 2 && rows / R < want && H % (R / 2) == 0) R /= 2;
-    return R;
+// rows per strip of the mixed row pass: the R dividing H that minimises (rounds of blocks over the chip)
+// x (R + 1) -- a strip of R rows inverts R + 1 row spectra (one halo row), and the blocks run in rounds
+// of (CUs x resident blocks per CU), so a short last round costs a whole one.  HD (1080 rows, 2 blocks of
+// 2 strips per CU): R = 15 -> 1,981 it/s against 1,910-1,927 with R = 8, and the model orders R = 8, 10,
+// 12, 15, 20, 24 as measured (profiles/r04_ab_hd_r.txt).  A/B knob ADMM_MIXED_R.
+int strip_rows_mixed(int H, long long rows, int N) {
+    if (const int e = env_int("ADMM_MIXED_R", 0); e > 0 && H % e == 0) return e;
+    const int sg = 256 / std::max(1, admm_mixed::row_lanes(N));  // strips per block
+    long long slots = 0;
+    {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                    hipSuccess)
+            slots = (long long)cus * std::max(1, admm_mixed::pass_a_blocks_per_cu(N));
+    }
+    if (slots <= 0) slots = 512;
+    int best = 1;
+    double best_t = 1e300;
+    for (int R = 1; R <= 32 && R <= H; ++R) {
+        if (H % R) continue;
+        const long long strips = rows / R;
+        const long long blocks = (strips + sg - 1) / sg;
+        const double t = (double)((blocks + slots - 1) / slots) * (R + 1);
+        if (t < best_t - 1e-9 || (t < best_t + 1e-9 && R > best)) {
+            best_t = t;
+            best = R;
+        }
+    }
+    return best;
 }
 
 // The inference solve of a smooth size (mixed_hw) on the fused two-pass iteration (mixed_kernels.hpp):
@@ -1620,7 +1643,7 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
         }
         if (int e = hchk(admm_mixed::r2c(N, bimg, spec[0], twW, rows, s), "k_row_r2c_m")) return e;  // r_1 = b
     }
-    const int R = strip_rows_mixed(H, rows, admm_mixed::row_lanes(N));
+    const int R = strip_rows_mixed(H, rows, N);
     int cur = 0, uin = 0;
     for (int it = 1; it <= d.maxit; ++it) {
         {

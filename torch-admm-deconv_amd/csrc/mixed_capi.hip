@@ -92,6 +92,19 @@ int row_lanes(int N) {
     });
     return l;
 }
+int pass_a_blocks_per_cu(int N) {
+    int nb = 0;
+    (void)with_row(N, [&](auto n) {
+        constexpr int NN = decltype(n)::value;
+        using G = MRowG<NN>;
+        if (lds(k_pass_a_m<NN, false, false>, G::lds_bytes()) != hipSuccess) return hipSuccess;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pass_a_m<NN, false, false>, G::NT, G::lds_bytes()) !=
+            hipSuccess)
+            nb = 0;
+        return hipSuccess;
+    });
+    return nb;
+}
 int col_cols(int H) {
     // the fewest columns a block may take: pass_b launches the plan's C, or 4 or 2 when N = W / 2 is no
     // multiple of it

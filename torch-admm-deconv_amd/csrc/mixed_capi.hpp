@@ -15,6 +15,7 @@ bool row_ok(int N);
 bool col_ok(int H);
 int col_cols(int H);  // the fewest columns per column-pass block (N must be a multiple)
 int row_lanes(int N);  // lanes of a row group (up to 256: several waves)
+int pass_a_blocks_per_cu(int N);  // resident 256-thread blocks of the row pass per CU (occupancy query)
 
 hipError_t r2c(int N, const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s);
 hipError_t c2r(int N, const cf* spec, float* img, const cf* twW, long long rows, hipStream_t s);

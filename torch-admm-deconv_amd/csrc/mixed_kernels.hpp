@@ -506,6 +506,9 @@ static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restri
 #ifndef ADMM_PASSB_M_WPE
 #define ADMM_PASSB_M_WPE 0
 #endif
+#ifndef ADMM_PASSB_M_LATEF  // 1: HD pass B 0.183 -> 0.160 ms, 1,790 -> 1,910 it/s (profiles/r04_ab_hd_latef.txt)
+#define ADMM_PASSB_M_LATEF 1
+#endif
 template <int H> constexpr int passb_m_wpe() { return (H & (H - 1)) == 0 ? 0 : ADMM_PASSB_M_WPE; }
 template <int H, int CC>
 __global__ void __launch_bounds__((MColG<H, CC>::NT)) __attribute__((amdgpu_waves_per_eu(passb_m_wpe<H>(), 0)))
@@ -530,16 +533,23 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM,
     cf v[EM];
 #pragma unroll
     for (int j = 0; j < Ec; ++j) v[j] = bload_cf(rs, voff, j * sstep);
-    __syncthreads();  // twiddles in LDS
-    mfft<H, Lc, EM, -1, 1, 1>(v, buf, tw, t, typename MCol<H>::Fwd{});
     // frequencies in layout(Rz): v[q + Qz k] <-> ky = t + Lc q + NBz k (valid for t + Lc q < NBz)
     float m[EM];
+    auto load_m = [&]() {
 #pragma unroll
-    for (int q = 0; q < Qz; ++q) {
-        const int vt = t + Lc * q;
+        for (int q = 0; q < Qz; ++q) {
+            const int vt = t + Lc * q;
 #pragma unroll
-        for (int k = 0; k < G::Rz; ++k) m[q + Qz * k] = (vt < NBz) ? fcM[(size_t)(vt + NBz * k) * (N + 1) + col] : 0.f;
-    }
+            for (int k = 0; k < G::Rz; ++k)
+                m[q + Qz * k] = (vt < NBz) ? fcM[(size_t)(vt + NBz * k) * (N + 1) + col] : 0.f;
+        }
+    };
+    // ADMM_PASSB_M_LATEF (A/B build knob): load the factors after the forward transform (fewer live
+    // registers through it) instead of issuing them with the data
+    if constexpr (!ADMM_PASSB_M_LATEF) load_m();
+    __syncthreads();  // twiddles in LDS
+    mfft<H, Lc, EM, -1, 1, 1>(v, buf, tw, t, typename MCol<H>::Fwd{});
+    if constexpr (ADMM_PASSB_M_LATEF) load_m();
     if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H - ky]
         __syncthreads();
 #pragma unroll
