@@ -254,8 +254,18 @@ template <int C> struct ColBuf {
     __device__ __forceinline__ cf& at(int i) const { return base[i * C]; }
 };
 
+// SYNC 1: a block barrier (__syncthreads: also waits for the wave's outstanding global loads);
+// SYNC 2: a block barrier for LDS traffic only, so global loads issued before it stay in flight across it
+// (the mixed pass B prefetches the next plane's columns through its inverse transform's exchanges)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 template <int SYNC> __device__ __forceinline__ void xsync() {
-    if constexpr (SYNC) {
+    if constexpr (SYNC == 2) {
+        lds_barrier();
+    } else if constexpr (SYNC) {
         __syncthreads();
     } else {
         // all lanes of a sub-group are in one wave: LDS ops of a wave execute
