@@ -149,7 +149,9 @@ template <int N> struct MRowG {
     static constexpr int EM = a > b ? a : b;
     static constexpr int NT = 256, SG = NT / Lg;
     static constexpr bool WIDE = Lg > 64;  // the row group spans several waves: LDS exchanges, block barriers
-    static constexpr int SYNC = WIDE ? 1 : 0;
+    // wide groups synchronise their LDS exchanges with LDS-only block barriers (fft_core xsync<2>): a
+    // __syncthreads would also drain the wave's outstanding global loads and stores at every exchange
+    static constexpr int SYNC = WIDE ? 2 : 0;
     static_assert(Lp * Ep == N && Ls * Es == N && Lp <= Lg && Ls <= Lg && Lg <= 256 && (Lg & (Lg - 1)) == 0,
                   "row plan");
     static_assert(sched_prod(typename P::Inv{}) == N && sched_prod(typename P::Fwd{}) == N, "row schedule");
@@ -324,12 +326,12 @@ template <int N> struct RowXfM {
     template <bool INV>
     __device__ __forceinline__ static void combine_lds(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
         const RowBuf buf = l.cur();
-        if (!G::PP) __syncthreads();  // one buffer: its previous readers are done
+        if (!G::PP) lds_barrier();  // one buffer: its previous readers are done
         if (t < Ls) {
 #pragma unroll
             for (int j = 0; j < Es; ++j) buf.at(t + Ls * j) = v[j];
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int j = 0; j < Es; ++j) {
             const int k = t + Ls * j;
@@ -380,7 +382,7 @@ template <int N> struct RowXfM {
             mfft_pp<N, Lg, EM, +1, 2>(v, l.base, RowBuf::slots(N), l.ph, tw, t, typename MRow<N>::Inv{});
         } else if constexpr (WIDE) {
             combine_lds<true>(v, l, tw, t);
-            mfft<N, Lg, EM, +1, 1, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Inv{});
+            mfft<N, Lg, EM, +1, SYNC, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Inv{});
         } else {
             combine<true>(v, tw, t);
             mfft<N, Lg, EM, +1, 0, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Inv{});
@@ -392,7 +394,7 @@ template <int N> struct RowXfM {
             mfft_pp<N, Lg, EM, -1, 2>(v, l.base, RowBuf::slots(N), l.ph, tw, t, typename MRow<N>::Fwd{});
             combine_lds<false>(v, l, tw, t);
         } else if constexpr (WIDE) {
-            mfft<N, Lg, EM, -1, 1, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Fwd{});
+            mfft<N, Lg, EM, -1, SYNC, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Fwd{});
             combine_lds<false>(v, l, tw, t);
         } else {
             mfft<N, Lg, EM, -1, 0, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Fwd{});
@@ -405,12 +407,12 @@ template <int N> struct RowXfM {
     __device__ __forceinline__ static void neighbour(const float (&val)[Ep], float (&out)[Ep], Lds& l, int t) {
         if constexpr (WIDE) {
             const RowBuf buf = l.cur();
-            if (!G::PP) __syncthreads();
+            if (!G::PP) lds_barrier();
             if (t < Lp) {
 #pragma unroll
                 for (int j = 0; j < Ep; ++j) buf.at(t + Lp * j).x = val[j];
             }
-            __syncthreads();
+            lds_barrier();
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
                 int k = t + Lp * j + SHIFT;
