@@ -100,9 +100,10 @@ int admm_tv_abi_version(void);
 const char* admm_tv_build_hash(void);
 
 /* 1: (H, W) runs on the fused power-of-two kernels (H in [16,4096], W in [16,2048]);
- * 3: a smooth size (2^a 3^b 5^c with a transform plan: W/2 in {240, 320, 360, 480, 540, 640, 960} or a
- *    power of two up to 1024, H in {240, 360, 480, 540, 720, 960, 1080, 2160} or a power of two up to
- *    4096, e.g. 1080x1920, 720x1280, 480x640): admm_tv_forward runs the same fused two-pass iteration
+ * 3: a smooth size (2^a 3^b 5^c with a transform plan: W/2 in {240, 320, 360, 400, 480, 540, 640, 720,
+ *    800, 960, 1280, 1920} or a power of two up to 2048, H in {240, 360, 480, 540, 600, 720, 768, 800,
+ *    960, 1080, 1200, 1440, 1536, 2160} or a power of two up to 4096, W/2 even, e.g. 1080x1920,
+ *    720x1280, 480x640, 2160x3840, 600x800): admm_tv_forward runs the same fused two-pass iteration
  *    with mixed-radix register transforms (ABI v6); the training forward / backward of these sizes
  *    run on the generic kernels, as for 2;
  * 2: any other size up to 65,536 points per side, run on the generic kernels (mixed-radix
