@@ -314,8 +314,13 @@ struct GRowInvMMArgs {
     int ldw;         // spectrum row pitch in complex values (>= Wh)
 };
 
+// occupancy target of the 256-thread row inverse (waves per SIMD; A/B build knob ADMM_GROW_INV_MM_W: 4 caps
+// its VGPRs at 128 so four blocks share a CU instead of three)
+#ifndef ADMM_GROW_INV_MM_W
+#define ADMM_GROW_INV_MM_W 3
+#endif
 template <int S, int NTH = 256>
-__global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 512 ? 4 : 3)))
+__global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 512 ? 4 : ADMM_GROW_INV_MM_W)))
 k_grow_inv_mm(GRowInvMMArgs a) {
     extern __shared__ __attribute__((aligned(16))) float F[];
     const int W = a.W, R = a.R, h = a.h, NL = a.NL, RP = a.RP, KS = a.KS, MT = a.MT, Wh = a.Wh;
