@@ -168,33 +168,11 @@ hipError_t iso_norm(int N, const IsoArgs& a, bool first, hipStream_t s) {
     });
 }
 
-// planes per pass-B block: the gp in [1, 8] minimising (rounds of blocks over the chip) x (gp + 1/2) --
-// a block's first plane load is exposed, its later planes' loads overlap the previous plane's inverse
-// transform.  A/B knob ADMM_PASSB_M_GP (read once per process).
-int passb_gp(long long P, int colblocks, long long slots) {
-    static const int forced = [] {
-        const char* e = std::getenv("ADMM_PASSB_M_GP");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (forced > 0) return (int)std::min<long long>(forced, std::max<long long>(P, 1));
-    int best = 1;
-    double best_t = 1e300;
-    for (int gp = 1; gp <= 8 && gp <= P; ++gp) {
-        const long long blocks = (P + gp - 1) / gp * colblocks;
-        const double t = (double)((blocks + slots - 1) / slots) * (gp + 0.5);
-        if (t < best_t - 1e-9) {
-            best_t = t;
-            best = gp;
-        }
-    }
-    return best;
-}
-
 hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s) {
     return with_col(H, [&](auto h) {
         constexpr int HH = decltype(h)::value;
-        // gp = 1: plane groups of two at H >= 1024 (k_pass_b's measured tile order), plane-major below;
-        // A/B knob ADMM_PASSB_M_ORDER (read once per process: it changes no sizes)
+        // plane groups of two at H >= 1024 (k_pass_b's measured tile order), plane-major below; A/B knob
+        // ADMM_PASSB_M_ORDER (read once per process: it changes no sizes)
         static const int forced = [] {
             const char* e = std::getenv("ADMM_PASSB_M_ORDER");
             return e ? std::atoi(e) : 0;
@@ -203,22 +181,10 @@ hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long 
         auto go = [&](auto cc) {
             constexpr int CC = decltype(cc)::value;
             using G = MColG<HH, CC>;
-            auto kern = k_pass_b_m<HH, CC>;
             const int colblocks = N / CC;
-            if (hipError_t e = lds(kern, G::lds_bytes_b())) return e;
-            static const long long slots = [&] {
-                int dev = 0, cus = 0, bpc = 0;
-                if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, G::NT, G::lds_bytes_b()) != hipSuccess)
-                    return 256LL;
-                return (long long)std::max(1, cus) * std::max(1, bpc);
-            }();
-            // plane groups only where the next plane can stream into LDS (G::PF)
-            const int gp = G::PF ? passb_gp(P, colblocks, slots) : 1;
-            const long long groups = (P + gp - 1) / gp;
-            hipLaunchKernelGGL(kern, dim3((unsigned)(groups * colblocks)), dim3(G::NT), G::lds_bytes_b(), s, spec, fcM,
-                               twH, N, colblocks, order, gp, (int)P);
+            if (hipError_t e = lds(k_pass_b_m<HH, CC>, G::lds_bytes())) return e;
+            hipLaunchKernelGGL((k_pass_b_m<HH, CC>), dim3((unsigned)(P * colblocks)), dim3(G::NT), G::lds_bytes(), s,
+                               spec, fcM, twH, N, colblocks, order);
             return hipGetLastError();
         };
         // the plan's columns per block, or fewer when N is no multiple of them (e.g. W = 1080 beside the

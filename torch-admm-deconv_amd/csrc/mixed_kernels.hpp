@@ -285,11 +285,6 @@ template <int H, int CC = MCol<H>::C> struct MColG {
     static_assert(sched_first(typename P::Inv{}) == Rz ||
                       (NBz % Lc == 0 && (H / sched_first(typename P::Inv{})) % Lc == 0), "column frequency layout");
     static constexpr size_t lds_bytes() { return sizeof(cf) * (H + (size_t)H * C); }
-    // pass B's next-plane prefetch buffer (global_load_lds: real and imaginary parts of each thread's Ec
-    // values, lane-linear) after the exchange buffer, where the LDS allows
-    static constexpr size_t pf_floats() { return (size_t)2 * Ec * ((NT + 63) / 64 * 64); }
-    static constexpr bool PF = lds_bytes() + sizeof(float) * pf_floats() <= 160 * 1024;
-    static constexpr size_t lds_bytes_b() { return lds_bytes() + (PF ? sizeof(float) * pf_floats() : 0); }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -516,136 +511,87 @@ static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restri
 #ifndef ADMM_PASSB_M_LATEF  // 1: HD pass B 0.183 -> 0.160 ms, 1,790 -> 1,910 it/s (profiles/r04_ab_hd_latef.txt)
 #define ADMM_PASSB_M_LATEF 1
 #endif
+// Measured and not kept (profiles/r04_ab_hd_passb_gp.txt): blocks walking 2-8 planes of their column
+// block with the next plane streamed into LDS (global_load_lds) during the inverse transform and
+// LDS-only barriers -- HD pass B 0.258-0.267 ms against 0.160 for one tile per block.
 template <int H> constexpr int passb_m_wpe() { return (H & (H - 1)) == 0 ? 0 : ADMM_PASSB_M_WPE; }
-// A block runs its column block through gp planes in turn (gp = 1: one tile, tile order `order`): the
-// twiddles and the Wiener factors are loaded once for all of them, and the next plane's columns stream
-// into LDS (global_load_lds, no registers) while the current plane's inverse transform runs -- a
-// 960-thread block is alone on its CU (112 VGPRs), so nothing else overlaps its loads with its
-// arithmetic.  The transform's exchanges use LDS-only barriers (xsync<2>) so the prefetch stays in flight.
 template <int H, int CC>
 __global__ void __launch_bounds__((MColG<H, CC>::NT)) __attribute__((amdgpu_waves_per_eu(passb_m_wpe<H>(), 0)))
-k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g, int N, int colblocks, int order,
-           int gp, int P) {
+k_pass_b_m(cf* spec, const float* __restrict__ fcM,
+                                                           const cf* __restrict__ twH_g, int N, int colblocks,
+                                                           int order) {
     using G = MColG<H, CC>;
-    constexpr int Lc = G::Lc, Ec = G::Ec, C = G::C, EM = G::EM, NBz = G::NBz, Qz = G::Qz, NT = G::NT;
-    constexpr int NTP = (NT + 63) / 64 * 64;  // prefetch buffer row: whole waves
+    constexpr int Lc = G::Lc, Ec = G::Ec, C = G::C, EM = G::EM, NBz = G::NBz, Qz = G::Qz;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
     cf* data = tw + H;
-    float* Bf = reinterpret_cast<float*>(data + (size_t)C * H);  // [Ec][2][NTP] (G::PF)
     load_tw(tw, twH_g, H);
     const int tid = threadIdx.x;
     const int c = tid % C, t = tid / C;
-    int p0, cb, np = 1;
-    if (gp <= 1 || !G::PF) {
-        pb_tile(xcd_remap(blockIdx.x, gridDim.x), colblocks, order, true, p0, cb);
-    } else {  // plane group major, adjacent column blocks (sharing 128-byte lines) adjacent
-        const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
-        p0 = (int)(lb / (unsigned)colblocks) * gp;
-        cb = (int)(lb % (unsigned)colblocks);
-        np = min(gp, P - p0);
-    }
+    int p, cb;
+    pb_tile(xcd_remap(blockIdx.x, gridDim.x), colblocks, order, true, p, cb);
     const int col = cb * C + c;
+    const rsrc_t rs = make_rsrc(spec + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
     const int voff = (t * N + col) * (int)sizeof(cf);
     const int sstep = Lc * N * (int)sizeof(cf);
-    const unsigned pbytes = (unsigned)((size_t)H * N * sizeof(cf));
-    // (the exchange buffer: ColBuf over data + c, re-derived per plane below)
+    ColBuf<C> buf{data + c};
     cf v[EM];
-    {
-        const rsrc_t rs = make_rsrc(spec + (size_t)p0 * H * N, pbytes);
 #pragma unroll
-        for (int j = 0; j < Ec; ++j) v[j] = bload_cf(rs, voff, j * sstep);
-    }
+    for (int j = 0; j < Ec; ++j) v[j] = bload_cf(rs, voff, j * sstep);
     // frequencies in layout(Rz): v[q + Qz k] <-> ky = t + Lc q + NBz k (valid for t + Lc q < NBz)
     float m[EM];
-    auto load_m = [&](int tt, const float* fm) {  // (tt, fm: t and fcM, opaque in the plane loop)
+    auto load_m = [&]() {
 #pragma unroll
         for (int q = 0; q < Qz; ++q) {
-            const int vt = tt + Lc * q;
+            const int vt = t + Lc * q;
 #pragma unroll
             for (int k = 0; k < G::Rz; ++k)
-                m[q + Qz * k] = (vt < NBz) ? fm[(size_t)(vt + NBz * k) * (N + 1) + col] : 0.f;
+                m[q + Qz * k] = (vt < NBz) ? fcM[(size_t)(vt + NBz * k) * (N + 1) + col] : 0.f;
         }
     };
     // ADMM_PASSB_M_LATEF (A/B build knob): load the factors after the forward transform (fewer live
     // registers through it) instead of issuing them with the data
-    if constexpr (!ADMM_PASSB_M_LATEF) load_m(t, fcM);
-    for (int pi = 0; pi < np; ++pi) {
-        const int p = p0 + pi;
-        // the lane indices and the bases re-derived opaquely per plane: otherwise the compiler hoists every
-        // exchange, factor and prefetch address of the plane out of the loop and spills them (432 B of
-        // scratch at 1080 rows)
-        int tl = t, tidl = tid;
-        cf* twp = tw;
-        cf* dp = data;
-        const float* fmp = fcM;
-        float* bfp = Bf;
-        asm volatile("" : "+v"(tl), "+v"(tidl), "+v"(twp), "+v"(dp), "+v"(fmp), "+v"(bfp));
-        if constexpr (G::PF) {
-            if (pi > 0) {  // this plane's columns arrived in the prefetch buffer
-                __builtin_amdgcn_s_waitcnt(0);
-                lds_barrier();
+    if constexpr (!ADMM_PASSB_M_LATEF) load_m();
+    __syncthreads();  // twiddles in LDS
+    mfft<H, Lc, EM, -1, 1, 1>(v, buf, tw, t, typename MCol<H>::Fwd{});
+    if constexpr (ADMM_PASSB_M_LATEF) load_m();
+    if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H - ky]
+        __syncthreads();
 #pragma unroll
-                for (int j = 0; j < Ec; ++j) v[j] = mkc(bfp[(2 * j) * NTP + tidl], bfp[(2 * j + 1) * NTP + tidl]);
+        for (int q = 0; q < Qz; ++q) {
+            const int vt = t + Lc * q;
+            if (vt < NBz) {
+#pragma unroll
+                for (int k = 0; k < G::Rz; ++k) buf.at(vt + NBz * k) = v[q + Qz * k];
             }
         }
-        lds_barrier();  // twiddles in LDS; the previous plane's inverse transform is done with buf
-        ColBuf<C> bl{dp + c};
-        mfft<H, Lc, EM, -1, 2, 1>(v, bl, twp, tl, typename MCol<H>::Fwd{});
-        // per plane (L2 hits after the first): factors held through the transforms would cost 16 VGPRs
-        // at their peak
-        if (ADMM_PASSB_M_LATEF) load_m(tl, fmp);
-        if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H - ky]
-            lds_barrier();
+        __syncthreads();
+        if (col == 0) {
 #pragma unroll
             for (int q = 0; q < Qz; ++q) {
-                const int vt = tl + Lc * q;
+                const int vt = t + Lc * q;
                 if (vt < NBz) {
 #pragma unroll
-                    for (int k = 0; k < G::Rz; ++k) bl.at(vt + NBz * k) = v[q + Qz * k];
-                }
-            }
-            lds_barrier();
-            if (col == 0) {
-#pragma unroll
-                for (int q = 0; q < Qz; ++q) {
-                    const int vt = tl + Lc * q;
-                    if (vt < NBz) {
-#pragma unroll
-                        for (int k = 0; k < G::Rz; ++k) {
-                            const int ky = vt + NBz * k;
-                            const cf qv = cconj(bl.at(ky == 0 ? 0 : H - ky));
-                            const float f0 = m[q + Qz * k], fn = fmp[(size_t)ky * (N + 1) + N];
-                            const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
-                            const cf x = v[q + Qz * k];
-                            v[q + Qz * k] = mkc(fmaf(a, x.x, b * qv.x), fmaf(a, x.y, b * qv.y));
-                        }
+                    for (int k = 0; k < G::Rz; ++k) {
+                        const int ky = vt + NBz * k;
+                        const cf qv = cconj(buf.at(ky == 0 ? 0 : H - ky));
+                        const float f0 = m[q + Qz * k], fn = fcM[(size_t)ky * (N + 1) + N];
+                        const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
+                        const cf x = v[q + Qz * k];
+                        v[q + Qz * k] = mkc(fmaf(a, x.x, b * qv.x), fmaf(a, x.y, b * qv.y));
                     }
                 }
             }
-            lds_barrier();  // the partner reads are done before the inverse transform reuses buf
         }
-        if (col != 0) {
-#pragma unroll
-            for (int i = 0; i < Qz * G::Rz; ++i) v[i] = cscale(v[i], m[i]);
-        }
-        if constexpr (G::PF) {
-            if (pi + 1 < np) {  // the next plane's columns -> LDS, in flight through the inverse transform
-                const float* nx = reinterpret_cast<const float*>(spec + (size_t)(p + 1) * H * N + (size_t)tl * N + col);
-                const int wb = tidl & ~63;
-#pragma unroll
-                for (int j = 0; j < Ec; ++j) {
-                    const float* src = nx + (size_t)2 * j * Lc * N;
-                    __builtin_amdgcn_global_load_lds(src, bfp + (2 * j) * NTP + wb, 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds(src + 1, bfp + (2 * j + 1) * NTP + wb, 4, 0, 0);
-                }
-            }
-        }
-        mfft<H, Lc, EM, +1, 2, 1>(v, bl, twp, tl, typename MCol<H>::Inv{});
-        const rsrc_t rs = make_rsrc(spec + (size_t)p * H * N, pbytes);
-#pragma unroll
-        for (int j = 0; j < Ec; ++j) bstore_cf(rs, voff, j * sstep, v[j]);
+        __syncthreads();  // the partner reads are done before the inverse transform reuses buf
     }
+    if (col != 0) {
+#pragma unroll
+        for (int i = 0; i < Qz * G::Rz; ++i) v[i] = cscale(v[i], m[i]);
+    }
+    mfft<H, Lc, EM, +1, 1, 1>(v, buf, tw, t, typename MCol<H>::Inv{});
+#pragma unroll
+    for (int j = 0; j < Ec; ++j) bstore_cf(rs, voff, j * sstep, v[j]);
 }
 
 // ---------------------------------------------------------------------------------------------
