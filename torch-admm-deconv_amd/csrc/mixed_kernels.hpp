@@ -188,9 +188,10 @@ template <> struct MCol<4096> : MColPow2<4096> {};
 #define ADMM_MCOL_C 8
 #endif
 // ADMM_M1080_V (A/B build knob): 0 = 120 threads x 9 values per column (960-thread blocks: one block per
-// CU at 112 VGPRs), 1 = 60 threads x 18 values (480-thread blocks: two per CU, twice the bytes in flight)
-#ifndef ADMM_M1080_V
-#define ADMM_M1080_V 0
+// CU at 112 VGPRs), 1 = 60 threads x 18 values (480-thread blocks: two per CU, twice the bytes in flight),
+// 2 = the 120 x 9 layout with the 9 * 12 * 10 schedule
+#ifndef ADMM_M1080_V  // 2: HD pass B 0.160 -> 0.120 ms, 62 VGPRs (profiles/r04_ab_hd_m1080s.txt)
+#define ADMM_M1080_V 2
 #endif
 template <> struct MCol<1080> {
 #if ADMM_M1080_V == 1
@@ -198,8 +199,13 @@ template <> struct MCol<1080> {
 #else
     static constexpr int Lc = 120, Ec = 9, C = ADMM_MCOL_C;
 #endif
+#if ADMM_M1080_V == 2  // 9 * 12 * 10: lanes busy 100 / 75 / 90 % per stage (9 * 15 * 8: 100 / 60 / 56 %), 12 values
+    using Fwd = Sched<9, 12, 10>;
+    using Inv = Sched<10, 12, 9>;
+#else
     using Fwd = Sched<9, 15, 8>;
     using Inv = Sched<8, 15, 9>;
+#endif
 };
 template <> struct MCol<2160> {
     static constexpr int Lc = 240, Ec = 9, C = 2;
