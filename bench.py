@@ -43,6 +43,10 @@ CONFIGS = {
             "generic-size path (row f4): batch-32 481x321x3 (BSD image size), 9x9 Gaussian PSF, aniso, 50 iters"),
     "hd": (8, 3, 1080, 1920, "gauss:1.5", 9, 50, False,
            "generic-size path (row f4): batch-8 1080x1920x3 (HD frame), 9x9 Gaussian PSF, aniso, 50 iters"),
+    "uhd": (2, 3, 2160, 3840, "gauss:2", 11, 50, False,
+            "smooth-size path (row f4): batch-2 2160x3840x3 (4K UHD frame), 11x11 Gaussian PSF, aniso, 50 iters"),
+    "sd": (32, 3, 360, 720, "gauss:1.5", 9, 50, False,
+           "smooth-size path (row f4): batch-32 360x720x3, 9x9 Gaussian PSF, aniso, 50 iters"),
     "c2": (32, 3, 512, 512, "motion", 15, 50, False,
            "C2: batch-32 512x512x3, 15x15 motion PSF, lambda 0.01, rho 0.02, aniso, 50 iters"),
     "c5fwd": (16, 3, 512, 512, "none", 0, 100, True,

@@ -207,10 +207,24 @@ template <> struct MCol<1080> {
     using Inv = Sched<8, 15, 9>;
 #endif
 };
+// ADMM_M2160_V / ADMM_M360_V (A/B build knobs): 1 = schedules that keep more lanes busy per guarded stage
+// (2160: 9 * 2 * 12 * 10, lanes 100 / 90 / 75 / 90 %, 12 values, one more exchange, vs 9 * 16 * 15 at
+// 100 / 56 / 60 %, 16 values; 360: 9 * 10 * 4 vs 9 * 8 * 5)
+#ifndef ADMM_M2160_V  // 1: 4K UHD pass B 0.2345 -> 0.214 ms (profiles/r04_ab_uhd_cols.txt)
+#define ADMM_M2160_V 1
+#endif
+#ifndef ADMM_M360_V  // 1: 360x720 pass B 0.0566 -> 0.0545 ms (profiles/r04_ab_sd_cols.txt)
+#define ADMM_M360_V 1
+#endif
 template <> struct MCol<2160> {
     static constexpr int Lc = 240, Ec = 9, C = 2;
+#if ADMM_M2160_V == 1
+    using Fwd = Sched<9, 2, 12, 10>;
+    using Inv = Sched<10, 12, 2, 9>;
+#else
     using Fwd = Sched<9, 16, 15>;
     using Inv = Sched<15, 16, 9>;
+#endif
 };
 template <> struct MCol<720> {
     static constexpr int Lc = 80, Ec = 9, C = ADMM_MCOL_C;
@@ -234,8 +248,13 @@ template <> struct MCol<480> {
 };
 template <> struct MCol<360> {
     static constexpr int Lc = 40, Ec = 9, C = 8;
+#if ADMM_M360_V == 1
+    using Fwd = Sched<9, 10, 4>;
+    using Inv = Sched<4, 10, 9>;
+#else
     using Fwd = Sched<9, 8, 5>;
     using Inv = Sched<5, 8, 9>;
+#endif
 };
 template <> struct MCol<240> {
     static constexpr int Lc = 16, Ec = 15, C = 8;
