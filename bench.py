@@ -45,6 +45,10 @@ CONFIGS = {
            "generic-size path (row f4): batch-8 1080x1920x3 (HD frame), 9x9 Gaussian PSF, aniso, 50 iters"),
     "uhd": (2, 3, 2160, 3840, "gauss:2", 11, 50, False,
             "smooth-size path (row f4): batch-2 2160x3840x3 (4K UHD frame), 11x11 Gaussian PSF, aniso, 50 iters"),
+    "p720": (16, 3, 720, 1280, "gauss:1.5", 9, 50, False,
+             "smooth-size path (row f4): batch-16 720x1280x3 (720p frame), 9x9 Gaussian PSF, aniso, 50 iters"),
+    "vga": (32, 3, 480, 640, "gauss:1.5", 9, 50, False,
+            "smooth-size path (row f4): batch-32 480x640x3 (VGA frame), 9x9 Gaussian PSF, aniso, 50 iters"),
     "sd": (32, 3, 360, 720, "gauss:1.5", 9, 50, False,
            "smooth-size path (row f4): batch-32 360x720x3, 9x9 Gaussian PSF, aniso, 50 iters"),
     "c2": (32, 3, 512, 512, "motion", 15, 50, False,

@@ -17,7 +17,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "torch-admm-deconv_amd", "csrc", "mixed_kernels.hpp")
-DEFAULTS = {"ADMM_M960_V": 0, "ADMM_M1080_V": 2, "ADMM_M2160_V": 1, "ADMM_M360_V": 1, "ADMM_MCOL_C": 8}
+DEFAULTS = {"ADMM_M960_V": 0, "ADMM_M1080_V": 2, "ADMM_M2160_V": 1, "ADMM_M360_V": 1, "ADMM_MROW_V": 1, "ADMM_MCOL_C": 8}
 
 
 def _preprocess(text):

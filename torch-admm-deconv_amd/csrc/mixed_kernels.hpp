@@ -87,21 +87,42 @@ template <> struct MRow<2048> {  // W = 4096: 256 lanes x 8 (4 waves)
     using Inv = Sched<8, 4, 8, 8>;
     using Fwd = Sched<8, 8, 4, 8>;
 };
+// ADMM_MROW_V (A/B build knob): 1 = 720p / VGA row schedules with fewer values per stage (640: 10 * 8 * 8
+// over 64 / 80 lanes, 320: 8 * 5 * 8 over 40 lanes)
+#ifndef ADMM_MROW_V  // 1: VGA pass A 0.201 -> 0.182 ms, 720p 0.333 -> 0.326 (profiles/r04_ab_vga_rows.txt, r04_ab_p720_rows.txt)
+#define ADMM_MROW_V 1
+#endif
+#if ADMM_MROW_V == 1
+template <> struct MRow<640> {  // W = 1280 (720p): spectra 64 x 10, pixels 80 x 8 (2 waves)
+    static constexpr int Lg = 128, Lp = 80, Ep = 8, Ls = 64, Es = 10;
+    using Inv = Sched<10, 8, 8>;
+    using Fwd = Sched<8, 8, 10>;
+};
+#else
 template <> struct MRow<640> {  // W = 1280 (720p): spectra 128 x 5, pixels 80 x 8 (2 waves)
     static constexpr int Lg = 128, Lp = 80, Ep = 8, Ls = 128, Es = 5;
     using Inv = Sched<5, 16, 8>;
     using Fwd = Sched<8, 16, 5>;
 };
+#endif
 template <> struct MRow<480> {  // W = 960: spectra 40 x 12, pixels 60 x 8
     static constexpr int Lg = 64, Lp = 60, Ep = 8, Ls = 40, Es = 12;
     using Inv = Sched<12, 5, 8>;
     using Fwd = Sched<8, 5, 12>;
 };
+#if ADMM_MROW_V == 1
+template <> struct MRow<320> {  // W = 640 (VGA): spectra 40 x 8, pixels 40 x 8
+    static constexpr int Lg = 64, Lp = 40, Ep = 8, Ls = 40, Es = 8;
+    using Inv = Sched<8, 5, 8>;
+    using Fwd = Sched<8, 5, 8>;
+};
+#else
 template <> struct MRow<320> {  // W = 640 (VGA): spectra 20 x 16, pixels 64 x 5
     static constexpr int Lg = 64, Lp = 64, Ep = 5, Ls = 20, Es = 16;
     using Inv = Sched<16, 4, 5>;
     using Fwd = Sched<5, 4, 16>;
 };
+#endif
 template <> struct MRow<240> {  // W = 480: spectra 16 x 15, pixels 30 x 8
     static constexpr int Lg = 32, Lp = 30, Ep = 8, Ls = 16, Es = 15;
     using Inv = Sched<15, 2, 8>;
