@@ -7,8 +7,10 @@ step   : one fft_admm_tv call over the rank's batch-64 shard (64x3x1024^2, 21x21
 value  : whole-job batch-64 ADMM iterations per second = n_gpus * 50 * K / T
          (T = max over ranks of the K-step wall time; weak scaling: 64 images per GPU).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL over xGMI).  Rank 0 prints ONE
+Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one process per GPU (RCCL
+over xGMI): under torch.distributed.run (the driver's launch; --gpus must equal WORLD_SIZE, else
+the bench exits with status 2), or, started without it, the bench starts torch.distributed.run
+itself as a child process before anything touches the GPU and exits with its status.  Rank 0 prints ONE
 JSON line with the roofline of the dominant kernel (HIP events on the launch
 stream inside the timed region) and the CPU baseline (the oracle, i.e. the
 reference's op sequence restated, timed on a bounded sample on the host cores).
@@ -82,7 +84,8 @@ BWD_ROW_BYTES, BWD_ROW_LAST_BYTES, BWD_ROW_FIRST_BYTES = 48, 36, 28
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under torch.distributed.run, else 1)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
@@ -93,6 +96,9 @@ def parse():
                          "the generic-size bsd / hd workloads, the training step)")
     ap.add_argument("--cpu-planes", type=int, default=6, help="CPU baseline sample: planes of 1024^2")
     ap.add_argument("--cpu-iters", type=int, default=36, help="CPU baseline sample: timed iterations")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="override the per-GPU batch (launch rehearsals only: the line then names a reduced "
+                         "workload, config.reduced_batch)")
     ap.add_argument("--c5-batch", type=int, default=None, help="C5 only: override the per-GPU batch")
     ap.add_argument("--c5-no-ckpt", action="store_true", help="C5 only: keep all branch activations")
     ap.add_argument("--c5-channels-last", action="store_true", help="C5 only: NHWC activations (MIOpen NHWC convs)")
@@ -370,7 +376,7 @@ def run_c5(args, world, rank, dev):
     from admmtor.modelbuild.denoiser import DivergentRestorer
     from admmtor.synth import CONFIG_SEED, clean_images
     B, C, H, W, _, _, maxit, _, desc = CONFIGS["c5"]
-    B = args.c5_batch or B
+    B = args.c5_batch or args.batch or B
     deconv = {"kern_size": (), "max_iters": maxit, "iso": True}
     torch.manual_seed(CONFIG_SEED + 5)
     model = DivergentRestorer([2, 8, 32], 3, 3, 86, 86, 8, output_activation=torch.nn.Sigmoid(),
@@ -457,9 +463,54 @@ def run_c5(args, world, rank, dev):
               flush=True)
 
 
+def resolve_world(gpus, env):
+    """(world size, launch ranks?) from --gpus and the environment, before any GPU call.
+    Under torch.distributed.run WORLD_SIZE is set and --gpus (if given) must equal it; without it,
+    --gpus N > 1 means this process launches the N ranks.  A mismatch raises SystemExit(2)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if gpus is not None and gpus != int(ws):
+            print(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws} (torch.distributed.run --nproc-per-node); "
+                  "they must be equal", file=sys.stderr, flush=True)
+            raise SystemExit(2)
+        return int(ws), False
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        print(f"bench.py: --gpus {n} must be >= 1", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    return n, n > 1
+
+
+def launch_cmd(n, argv, port):
+    """The child that runs the N ranks: torch.distributed.run on this same script, on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """Start the N rank processes as ONE child process tree (torch.distributed.run) and return its
+    exit status.  Called before this process touches the GPU (torch.cuda.device_count() does not
+    initialise it on this image), and the ranks are children, never an exec of this process."""
+    import socket
+    import subprocess
+    rehearsal = bool(os.environ.get("ADMM_BENCH_REHEARSAL"))
+    ndev = torch.cuda.device_count()
+    if not rehearsal and n > ndev:
+        print(f"bench.py: --gpus {n} but {ndev} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    print(f"bench.py: launching {n} ranks (torch.distributed.run, port {port})", file=sys.stderr, flush=True)
+    return subprocess.run(launch_cmd(n, argv, port), env=env).returncode
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, launch = resolve_world(args.gpus, os.environ)
+    if launch:
+        sys.exit(launch_ranks(world, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -476,6 +527,8 @@ def main():
             dist.destroy_process_group()
         return
     cfg = CONFIGS[args.config]
+    if args.batch is not None:  # launch rehearsals only; the line names the reduced workload
+        cfg = (args.batch,) + cfg[1:8] + (cfg[8] + f" [REDUCED: batch {args.batch} per GPU]",)
     B, C, H, W, kind, k, maxit, iso, desc = cfg
 
     from admmtor import _native
@@ -623,7 +676,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (piecewise-constant shapes, circular blur, AWGN 0.01; seeded per rank)",
-            "config": {"workload": desc, "batch_per_gpu": B, "channels": C, "H": H, "W": W, "psf": f"{kind}/{k}",
+            "config": {"workload": desc, "batch_per_gpu": B, "reduced_batch": args.batch is not None, "channels": C, "H": H, "W": W, "psf": f"{kind}/{k}",
                        "maxit": maxit, "iso": iso,
                        "parallelism": (f"shard{world} (batch sharded; RCCL broadcast of PSF/lambda/rho per step and "
                                        "the final all_gather of every step's output inside the timed region, on a "

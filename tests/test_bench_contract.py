@@ -54,3 +54,36 @@ def test_cpu_baseline_leg_small_sample():
     res = bench.cpu_baseline(cfg, planes=3, iters=2)
     assert res["kind"] == "port" and res["value"] > 0 and res["cores"] >= 1
     assert "planes 3/6" in res["sample"] and res["unit"] == "batch-equivalent ADMM iterations/s"
+
+
+def test_world_from_gpus_and_env():
+    """--gpus N without torch.distributed.run launches N ranks; under it, --gpus must equal WORLD_SIZE."""
+    assert bench.resolve_world(None, {}) == (1, False)
+    assert bench.resolve_world(1, {}) == (1, False)
+    assert bench.resolve_world(8, {}) == (8, True)
+    assert bench.resolve_world(None, {"WORLD_SIZE": "4"}) == (4, False)
+    assert bench.resolve_world(4, {"WORLD_SIZE": "4"}) == (4, False)
+    for gpus, env in ((8, {"WORLD_SIZE": "1"}), (2, {"WORLD_SIZE": "4"}), (0, {})):
+        with pytest.raises(SystemExit) as e:
+            bench.resolve_world(gpus, env)
+        assert e.value.code == 2
+
+
+def test_launch_cmd_is_torchrun_on_loopback():
+    cmd = bench.launch_cmd(8, ["--gpus", "8", "--steps", "3"], 29511)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29511"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+def test_gpus_mismatch_exits_before_any_gpu_call():
+    """A torchrun rank whose --gpus differs from WORLD_SIZE exits with status 2 at once (no JSON line)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2, p.stderr
+    assert p.stdout.strip() == "" and "WORLD_SIZE=2" in p.stderr

@@ -140,21 +140,39 @@ def test_admmdeconv_training_step_c5_shape(cuda_dev):
 
 def test_input_modified_in_place_after_forward(cuda_dev):
     """The reference's graph keeps no reference to xin (its circular pad copies), so a caller may
-    change xin in place between the forward and the backward.  The native op keeps a private copy of
-    an x that does not require grad: same gradients as without the modification."""
+    change xin in place between the forward and the backward: same gradients as without the
+    modification.  Without a PSF gradient the native backward does not read x (only referenced);
+    with one the op keeps a private copy.  A double backward, which rebuilds the iteration from x,
+    raises after such a modification instead of differentiating another input."""
     from admmtor.eops.deconv import fft_admm_tv
-    from admmtor.synth import blurred_batch
+    from admmtor.synth import blurred_batch, make_psf
     x = blurred_batch(2, 3, 64, 64, torch.empty(0), seed=4).to(cuda_dev)
-    grads = []
-    for modify in (False, True):
+    for with_psf in (False, True):
+        grads = []
+        for modify in (False, True):
+            xi = x.clone()
+            lam = torch.tensor([0.02], device=cuda_dev, requires_grad=True)
+            rho = torch.tensor([0.05], device=cuda_dev, requires_grad=True)
+            k = (make_psf("motion", 5).to(cuda_dev).requires_grad_(True) if with_psf
+                 else torch.empty(0, device=cuda_dev))
+            params = (lam, rho, k) if with_psf else (lam, rho)
+            out = fft_admm_tv(xi, lam, rho, k, True, 10)
+            if modify:
+                xi.add_(1.0)
+            grads.append(torch.autograd.grad(out.square().sum(), params))
+        assert all(torch.equal(a, b) for a, b in zip(*grads)), with_psf
+    for early in (False, True):  # modified before / after the first backward
         xi = x.clone()
         lam = torch.tensor([0.02], device=cuda_dev, requires_grad=True)
-        rho = torch.tensor([0.05], device=cuda_dev, requires_grad=True)
-        out = fft_admm_tv(xi, lam, rho, torch.empty(0, device=cuda_dev), True, 10)
-        if modify:
-            xi.add_(1.0)
-        grads.append(torch.autograd.grad(out.square().sum(), (lam, rho)))
-    assert all(torch.equal(a, b) for a, b in zip(*grads))
+        out = fft_admm_tv(xi, lam, 0.05, torch.empty(0, device=cuda_dev), False, 5)
+        if early:
+            xi.mul_(2.0)
+        (gl,) = torch.autograd.grad(out.square().sum(), lam, create_graph=True)
+        if not early:
+            torch.autograd.grad(gl.sum(), lam, retain_graph=True)  # unmodified: the double backward runs
+            xi.mul_(2.0)
+        with pytest.raises(RuntimeError, match="modified"):
+            torch.autograd.grad(gl.sum(), lam)
 
 
 def hip_grads_psf(x, psf, lam, rho, iso, it, cot, dev):

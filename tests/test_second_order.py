@@ -105,3 +105,25 @@ def test_unrolled_solve_grouped_modules():
     for g in range(2):
         one = unrolled_solve(d["x"], lam[g:g + 1], rho[g:g + 1], psf, True, maxit)
         assert torch.equal(both[g * B:(g + 1) * B], one)
+
+
+@pytest.mark.parametrize("flat", [True, False])
+@pytest.mark.parametrize("iso", [False, True])
+def test_tangent_solve_matches_jvp_of_unrolled_lam0(flat, iso):
+    """tangent_solve (the default second-order path) is the directional derivative torch's forward
+    mode takes through unrolled_solve, also with lam = 0 on flat regions (a = 0 and tau = 0: the soft
+    threshold passes its clamp, and torch's derivative of sign(a)*clamp_min(|a|-tau, 0) is 0 there)."""
+    from admmtor._unrolled import tangent_solve
+    g = torch.Generator().manual_seed(11)
+    x = torch.zeros(2, 2, 12, 16, dtype=torch.float64)
+    if not flat:
+        x = torch.rand(x.shape, generator=g, dtype=torch.float64)
+    tx = torch.randn(x.shape, generator=g, dtype=torch.float64)
+    lam = torch.tensor([0.0], dtype=torch.float64)
+    rho = torch.tensor([0.05], dtype=torch.float64)
+    tl, tr = torch.tensor([0.3], dtype=torch.float64), torch.tensor([0.01], dtype=torch.float64)
+    psf = torch.empty(0, dtype=torch.float64)
+    y, ydot = tangent_solve(x, lam, rho, psf, iso, 6, (tx, tl, tr, None))
+    y2, ydot2 = torch.func.jvp(lambda a, b, c: unrolled_solve(a, b, c, psf, iso, 6), (x, lam, rho), (tx, tl, tr))
+    assert torch.equal(y, y2)
+    assert rel_l2(ydot, ydot2) <= 1e-12

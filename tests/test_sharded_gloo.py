@@ -183,3 +183,58 @@ def test_host_group_of_a_subgroup_world3():
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = dict(q.get(timeout=5) for _ in range(world))
     assert res == {0: [10, 11], 1: [10, 11], 2: None}
+
+
+def _subgroup_then_world_worker(rank, world, port, q):
+    """A subgroup host group (ranks 0, 1 only) is created first, then the world's host group on every
+    rank: the world group must not be named from per-rank state (torch's hashed names count the groups
+    the calling rank knows, which differ between ranks 0/1 and 2/3 here), or ranks would rendezvous
+    under different names and hang."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "torch-admm-deconv_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=__import__("datetime").timedelta(seconds=60))
+    try:
+        from admmtor import sharded
+
+        def sizes(v, hg, n):  # what shard_sizes does on a host group (with an RCCL `group`)
+            parts = [torch.zeros(1, dtype=torch.int64) for _ in range(n)]
+            dist.all_gather(parts, torch.tensor([v], dtype=torch.int64), group=hg)
+            return [int(p[0]) for p in parts]
+        sub = dist.new_group(ranks=[0, 1])
+        out = {}
+        if rank in (0, 1):
+            out["sub"] = sizes(3 + rank, sharded.make_host_group(sub), 2)
+        out["world"] = sizes(5 + rank, sharded.make_host_group(None), 4)   # every rank
+        if rank in (2, 3):  # a second subgroup created after the world group, by its own members
+            sub2 = dist.new_group(ranks=[2, 3], use_local_synchronization=True)
+            out["sub2"] = sizes(7 + rank, sharded.make_host_group(sub2), 2)
+        q.put((rank, out))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_group_subgroup_first_then_world_world4():
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_then_world_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import time
+    deadline = time.monotonic() + 120  # a naming mismatch hangs the ranks: bound the whole wait
+    for p in procs:
+        p.join(max(0.0, deadline - time.monotonic()))
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert all(c == 0 for c in codes), codes
+    res = dict(q.get(timeout=5) for _ in range(world))
+    for r in range(4):
+        assert res[r]["world"] == [5, 6, 7, 8]
+    assert res[0]["sub"] == res[1]["sub"] == [3, 4]
+    assert res[2]["sub2"] == res[3]["sub2"] == [9, 10]

@@ -187,15 +187,26 @@ def _setup_context(ctx, inputs, output):
     # x: read by the native backward only for the PSF gradient (b = H_t(x) path), and by a double
     # backward (admmtor._unrolled rebuilds the iteration from it).  An x that requires grad is saved
     # as itself (the double backward must reach it; autograd's usual version check applies, as for
-    # any op that saves its input).  Otherwise a private copy is kept: the reference's graph saves no
-    # reference to xin (its circular pad copies), so a caller may still modify xin in place after
-    # the forward and call backward (one image of memory next to the 2 K images of history).
-    xs = x if x.requires_grad else x.detach().clone()
+    # any op that saves its input).  The reference's graph saves no reference to xin (its circular pad
+    # copies), so a caller may modify xin in place after the forward and still call backward: with a
+    # PSF gradient a private copy is kept (one image next to the 2 K images of history); otherwise x
+    # is only referenced with its version, the first-order backward does not read it, and a double
+    # backward after such a modification raises instead of differentiating the wrong input.
+    ctx.xref = None
+    if x.requires_grad:
+        xs = x
+    elif psf_grad:
+        xs = x.detach().clone()
+    else:
+        xs = x.new_empty(0)
+        ctx.xref = (x.detach(), x._version)
     ctx.save_for_backward(xs, lam, rho, kern, hist)
 
 
 def _backward(ctx, gout, ghist):
     x, lam, rho, kern, hist = ctx.saved_tensors
+    if ctx.xref is not None and ctx.xref[0]._version == ctx.xref[1]:
+        x = ctx.xref[0]  # unmodified since the forward (else x stays empty: no double backward)
     need_x = ctx.needs_input_grad[0]
     need_s = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
     need_k = ctx.needs_input_grad[3] and kern.numel() > 0

@@ -119,11 +119,12 @@ def unrolled_solve(xin: Tensor, lam: Tensor, rho: Tensor, kern: Tensor, iso: boo
 # ---------------------------------------------------------------------------------------------
 def _soft_dual(a: Tensor, da: Tensor, tau: Tensor, dtau: Tensor) -> Tuple[Tensor, Tensor]:
     """soft threshold and its tangent, with torch's derivative conventions for the same expression
-    (clamp_min passes the gradient at equality, sign has none)."""
+    (clamp_min passes the gradient at equality, sign has none, abs has sign(a) -- so 0 at a = 0, where
+    tau <= 0 still passes the clamp)."""
     sg = torch.sign(a)
     m = torch.abs(a) - tau
     z = sg * torch.clamp_min(m, 0.0)
-    dz = torch.where(m >= 0, da - sg * dtau, torch.zeros_like(da))
+    dz = torch.where(m >= 0, sg * sg * da - sg * dtau, torch.zeros_like(da))
     return z, dz
 
 
@@ -282,7 +283,8 @@ def double_backward(gout: Tensor, x: Tensor, lam: Tensor, rho: Tensor, kern: Ten
     outer = torch.is_grad_enabled()
     none = (None,) * 5
     if x.numel() == 0:
-        raise RuntimeError("admmtor: double backward needs the forward's input x (not kept by this call)")
+        raise RuntimeError("admmtor: double backward needs the forward's input x, which was modified in place "
+                           "after the forward (or not kept by this call)")
     import os
     if not outer and os.environ.get("ADMM_SO_UNROLLED", "0") == "0":
         # the usual second order (no graph of the result needed): the tangent formulation, checkpointed

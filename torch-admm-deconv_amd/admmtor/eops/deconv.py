@@ -186,10 +186,11 @@ def fft_admm_tv(xin: torch.Tensor,
 # A line whose length has a prime factor R beyond Bluestein's reach (2R - 1 > 1024, or any R on lines
 # longer than 10,240 points) runs that factor as an any-prime stage: every output a sum of R terms, O(R)
 # per output.  In fp32 those sums lose accuracy as R grows (13,001: 7.1e-6 vs the fp64 oracle, the 1e-5
-# gate close); fp32 solves with a prime factor above this bound therefore compute in fp64 (the generic
-# kernels' double instantiation) and return fp32 -- same kernels, same cost order (O(n R) per line),
-# fp64 accuracy.  tests/test_gpu_generic.py runs 65,521, the largest prime line accepted.
-F32_MAX_PRIME = 16384
+# gate close); fp32 solves with a prime factor above this bound -- the largest prime measured in fp32 --
+# therefore compute in fp64 (the generic kernels' double instantiation) and return fp32: same kernels,
+# same cost order (O(n R) per line), fp64 accuracy.  tests/test_gpu_generic.py runs 13,001 in fp32 and
+# 13,003 / 16,381 / 65,521 (the largest prime line accepted) through fp64.
+F32_MAX_PRIME = 13001
 
 
 def _largest_prime(n: int) -> int:

@@ -140,15 +140,21 @@ def _group_key(group):
 def make_host_group(group=None):
     """The CPU (gloo) group over the ranks of `group` that ``shard_sizes`` exchanges sizes on.
 
-    Created with ``use_local_synchronization=True``: only the member ranks of `group` enter the
-    creation (``new_group`` is otherwise a collective over the whole default world, so a subgroup's
-    first gather would hang waiting for the ranks outside it).  Cached per rank set.  Callers that
-    prefer to build it up front (e.g. right after creating `group`, on its members) may call this
-    once; ``shard_sizes`` otherwise creates it on first use."""
+    The world (``group=None`` or a group over every rank) gets an ordinary ``new_group``: a
+    collective of all ranks, named from torch's group counter, which advances on every rank alike.
+    A true subgroup is created with ``use_local_synchronization=True``, so only its members enter
+    the creation (a plain ``new_group`` is a collective over the whole world, and a subgroup's first
+    gather would hang waiting for the ranks outside it).  torch names such a group by hashing its
+    ranks with the number of groups the calling rank already knows, so two members that have seen
+    different groups before would rendezvous under different names: create subgroup host groups up
+    front, right after the subgroups themselves, in the same order on every rank (calling this
+    function on each member).  Cached per rank set; ``shard_sizes`` otherwise creates it on first use."""
     key = _group_key(group)
     if key not in _size_groups:
-        ranks = None if group is None else list(key)
-        _size_groups[key] = dist.new_group(ranks=ranks, backend="gloo", use_local_synchronization=True)
+        if key == tuple(range(dist.get_world_size())):
+            _size_groups[key] = dist.new_group(backend="gloo")
+        else:
+            _size_groups[key] = dist.new_group(ranks=list(key), backend="gloo", use_local_synchronization=True)
     return _size_groups[key]
 
 
