@@ -72,10 +72,6 @@ ISO_NORM_BYTES = 12
 # generic sizes: the column pass (half spectra in and out, 8) and the inverse row transform that
 # follows it in the same timer (half spectra in 4, x image out 4)
 GEN_COL_BYTES = 16
-# ... and with the fused row pass (aniso inference at row lengths with a matrix-core plan,
-# csrc/gfused_mm.hpp): the column pass alone (8) per iteration, the row inverse (8) only after the last
-# one, each in its own timer scope; the fused row pass moves pass A's 28 B/px (spectrum in for x)
-GEN_COL_FUSED_BYTES = 8
 # training backward, reverse row pass (admm_backward.hpp k_bwd_pass_a) per reverse step k: reads the
 # r^ spectrum 4, a^_k 8, a_k 8, a_{k-1} 8, b^ 4; writes b^ 4, a^_{k-1} 8, the x^ spectrum 4 = 48;
 # k = K reads no a^ and no b^ (36); k = 1 reads no a_{k-1} and writes no a^ / x^ (28)
@@ -210,15 +206,10 @@ def generic_extras(dev, no_parity, keys=("bsd", "hd")):
             else:
                 os.environ["ADMM_GEN_STREAMS"] = old
         generic = e["path"] == "generic"  # the fused paths (power-of-two and mixed-radix) keep pass A / B bytes
-        # generic with the fused row pass: maxit + 1 column-phase scopes per solve (column passes + the
-        # final row inverse) instead of maxit (column pass + row inverse each)
-        fused_rows = generic and not iso and cnt[1] == 2 * (maxit + 1)
-        if fused_rows:
-            e["path"] = "generic, fused row pass"
         ba = (2 * PASS_A_FIRST_BYTES + (cnt[0] - 2) * PASS_A_BYTES) * npx
-        bb = cnt[1] * ((GEN_COL_FUSED_BYTES if fused_rows else GEN_COL_BYTES) if generic else PASS_B_BYTES) * npx
+        bb = cnt[1] * (GEN_COL_BYTES if generic else PASS_B_BYTES) * npx
         per = {}
-        for name, t, n, b in ((("fused_row_pass" if fused_rows else "row_step") if generic else "pass_a", ms[0], cnt[0], ba),
+        for name, t, n, b in (("row_step" if generic else "pass_a", ms[0], cnt[0], ba),
                               ("column_pass" if generic else "pass_b", ms[1], cnt[1], bb)):
             gbs = b / (t / 1e3) / 1e9 if t > 0 else None
             per[name] = {"avg_launch_ms": t / max(n, 1), "launches": n, "algorithmic_bytes_per_launch": b / max(n, 1),
@@ -535,6 +526,11 @@ def main():
     from admmtor.sharded import sharded_fft_admm_tv
     from admmtor.synth import CONFIG_SEED, blurred_batch, make_psf
 
+    def progress(msg):  # multi-rank runs: rank 0's stages on stderr (a slow start stays visible)
+        if world > 1 and rank == 0:
+            print(f"bench rank 0/{world}: {msg}", file=sys.stderr, flush=True)
+
+    progress("process group up")
     # rank-local shard of synthetic blurred images, generated directly in HBM
     psf = make_psf(kind, k).to(dev) if k else torch.empty(0, device=dev)
     x = blurred_batch(B, C, H, W, psf.cpu(), seed=CONFIG_SEED + 2 + 1000 * rank, device=dev)
@@ -567,11 +563,13 @@ def main():
             out.record_stream(comm)
         return out
 
+    progress("inputs ready")
     for _ in range(args.warmup):
         out = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    progress("warm-up done")
     _native.profile_reset()
     _native.profile_enable(True)
     torch.cuda.synchronize()
@@ -590,6 +588,7 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     T = elapsed.item()
+    progress(f"timed region done ({T:.2f} s)")
 
     P = B * C
     npx = P * H * W
@@ -624,11 +623,9 @@ def main():
     na = cnt[0]
     bytes_a = ((roof_steps * PASS_A_FIRST_BYTES + (na - roof_steps) * PASS_A_BYTES) * npx if na >= roof_steps
                else na * PASS_A_BYTES * npx)
-    # generic aniso inference with the fused row pass: maxit + 1 column-phase scopes per solve (8 B/px each)
-    fused_rows = generic and not iso and cnt[1] == roof_steps * (maxit + 1)
-    gen_col = GEN_COL_FUSED_BYTES if fused_rows else GEN_COL_BYTES
+    gen_col = GEN_COL_BYTES
     bytes_b = cnt[1] * (gen_col if generic else PASS_B_BYTES) * npx
-    names = (("fused_row_pass" if fused_rows else "row_step"), "column_pass") if generic else ("pass_a", "pass_b")
+    names = ("row_step", "column_pass") if generic else ("pass_a", "pass_b")
     kern = {
         names[0]: (ms[0], na, bytes_a),
         names[1]: (ms[1], cnt[1], bytes_b),

@@ -175,3 +175,54 @@ def test_supported_sizes():
     assert small < (16 << 20)  # one 12,000-point row: one slot, not 1,024
     big = nat.workspace_size(nat.desc(2, 3, 12000, 12000, 0, False, 5))
     assert big >= 7 * 2 * 3 * 12000 * 12000 * 4
+
+
+# ---------------------------------------------------------------- frozen release library
+CSRC = os.path.join(ROOT, "torch-admm-deconv_amd", "csrc")
+RUNTIME_SETTINGS = {"ADMM_GEN_STREAMS"}  # documented in INTEGRATION.md (and csrc/knobs.hpp)
+
+
+def _sources():
+    for name in sorted(os.listdir(CSRC)):
+        if name.endswith((".hip", ".hpp")):
+            yield name, open(os.path.join(CSRC, name)).read()
+
+
+def test_environment_reads_are_gated():
+    """Every environment read of the library goes through knobs.hpp: getenv nowhere else; the
+    env_setting names (read in every build) are exactly the documented runtime settings; every other
+    name is an env_int A/B knob, which a release build (no -DADMM_AB_BUILD) compiles to its default."""
+    settings, knobs = set(), set()
+    for name, txt in _sources():
+        code = re.sub(r"//[^\n]*", "", txt)
+        if name != "knobs.hpp":
+            assert "getenv" not in code, f"{name}: environment read outside knobs.hpp"
+            assert "secure_getenv" not in code and "environ" not in code.replace("environment", ""), name
+        settings |= set(re.findall(r'env_setting\(\s*"(ADMM_\w+)"', code))
+        knobs |= set(re.findall(r'env_int\(\s*"?(ADMM_\w+|knob)', code))
+    assert settings == RUNTIME_SETTINGS, settings
+    knobs_hpp = open(os.path.join(CSRC, "knobs.hpp")).read()
+    assert re.search(r"inline int env_int\(const char\* name, int dflt\) \{ return ADMM_AB_BUILD \?", knobs_hpp)
+    assert re.search(r"#ifndef ADMM_AB_BUILD\s*#define ADMM_AB_BUILD 0", knobs_hpp)
+    mk = open(os.path.join(CSRC, "Makefile")).read()
+    assert "ADMM_AB_BUILD" not in mk  # the release build never turns the knobs on
+    assert all(s in knobs_hpp for s in RUNTIME_SETTINGS)
+    integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert all(s in integ for s in RUNTIME_SETTINGS)
+
+
+def test_release_library_ignores_ab_knobs():
+    """The workspace layout depends on A/B knobs (the spectrum pitch, the mixed-radix path, the iso
+    plane groups): in the release library, setting them changes nothing."""
+    import sys
+    code = ("import sys; sys.path[:0] = [%r]\n"
+            "from admmtor import _native\n"
+            "for hw in ((321, 481), (1080, 1920), (512, 512)):\n"
+            "    for iso in (0, 1):\n"
+            "        d = _native.AdmmTvDesc(B=4, C=3, H=hw[0], W=hw[1], kh=9, kw=9, iso=iso, maxit=5)\n"
+            "        print(_native.workspace_size(d))\n") % os.path.join(ROOT, "torch-admm-deconv_amd")
+    env0 = {k: v for k, v in os.environ.items() if not k.startswith("ADMM_")}
+    env1 = dict(env0, ADMM_GEN_PITCH="0", ADMM_MIXED="0", ADMM_ISO_PPG="1", ADMM_GCOL_MM="0", ADMM_GROW_MM="0")
+    outs = [subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, check=True).stdout
+            for e in (env0, env1)]
+    assert outs[0] == outs[1] and len(outs[0].split()) == 6

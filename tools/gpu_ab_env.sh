@@ -1,5 +1,6 @@
 #!/bin/bash
-# Interleaved A/B of environment knobs on one bench config: bench.py --config <cfg> for each setting, two
+# Interleaved A/B of environment knobs on one bench config (the knobs are read only by an A/B build of the
+# library, csrc/knobs.hpp: bash tools/build_variant.sh ab, then ADMMTOR_LIB_OVERRIDE=tools/_variants/ab.so): bench.py --config <cfg> for each setting, two
 # rounds, each run under its own time limit; the bench's JSON line (value, roofline) per run.
 # usage: bash tools/gpu_ab_env.sh <config> "A=1 B=2" "A=0 B=2" ...   -> gpurun_out/ab_env_<config>.txt
 set -o pipefail

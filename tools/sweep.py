@@ -1,4 +1,6 @@
 """In-process tuning sweep of the HIP passes (ADMM_PASSB_C / ADMM_PASSA_R env knobs).
+The knobs are read only by an A/B build of the library (csrc/knobs.hpp): bash tools/build_variant.sh ab,
+then run with ADMMTOR_LIB_OVERRIDE=tools/_variants/ab.so.
 
 usage: python tools/sweep.py [--config c3] [--steps 3] VAR=v1,v2 [VAR2=...]
 Prints per-kernel average launch time and GB/s (algorithmic bytes) for each setting.

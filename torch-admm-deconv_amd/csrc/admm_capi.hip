@@ -15,7 +15,7 @@
 #include <vector>
 
 #include "gcol_mm.hpp"
-#include "gfused_mm.hpp"
+#include "knobs.hpp"
 #include "mixed_capi.hpp"
 #include "admm_tv.h"
 
@@ -106,7 +106,6 @@ bool generic_hw(int64_t H, int64_t W) {
     return !supported_hw(H, W) && H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax && gen_fits((int)H) &&
            gen_fits((int)W);
 }
-int env_int(const char* name, int dflt);
 // smooth sizes on the fused two-pass iteration with mixed-radix register transforms (mixed_kernels.hpp,
 // DESIGN.md §7c): W even with a row plan for W / 2, a column plan for H, not both powers of two (those
 // are supported_hw).  Inference only: the training forward / backward of these sizes stay generic.
@@ -122,11 +121,6 @@ bool f64_hw(int64_t H, int64_t W) {
     return H >= 1 && W >= 1 && H <= kGenericMax && W <= kGenericMax && gen_fits((int)H, true) && gen_fits((int)W, true);
 }
 
-int env_int(const char* name, int dflt) {
-    const char* s = std::getenv(name);
-    return s ? std::atoi(s) : dflt;
-}
-
 GPlan make_plan(int n, bool f64 = false);  // generic-size transform plan (below)
 size_t glb_scratch(int H, int W, long long P, bool f64);  // long lines' scratch bytes (below)
 // matrix-core column pass (gcol_mm.hpp): H = S R, odd R in [17, 127] carrying H's largest prime
@@ -139,14 +133,6 @@ struct MMPlan {
 };
 MMPlan mm_plan(int H, int W);
 MMPlan mm_plan_row(int W);  // the row inverse (k_grow_inv_mm): W = S R, S in {1..5, 8, 13}
-// the fused row pass of aniso inference (gfused_mm.hpp): the row plan's S, R; strips of up to 2 NLf rows
-struct FusedPlan {
-    bool ok;
-    int S, R, h, KS, MT, NLi, RPi, NLf, RPf, nth;
-    int regA, offX, offT;  // LDS regions (floats)
-    size_t lds;
-};
-FusedPlan fused_plan(const MMPlan& row, int W);
 
 // modules solved together (admm_tv_desc.groups)
 int ngroups_of(const admm_tv_desc& d) { return d.groups > 1 ? d.groups : 1; }
@@ -159,7 +145,6 @@ struct Layout {
     // generic path: the matrix-core plans, decided once per call (their environment knobs are read
     // here only, so the regions sized below and the kernels launched later always agree)
     MMPlan mm, mmr;
-    FusedPlan fz;  // aniso inference: the fused row pass (ok = false: step pass + row inverse)
     // mixed-radix fused inference (mixed_hw; run_forward_mixed): the Wiener factor for its column pass
     bool mixed;
     size_t fcM;
@@ -192,16 +177,14 @@ Layout make_layout(const admm_tv_desc& d) {
     if (L.gen && !f64) {
         L.mm = mm_plan((int)H, (int)W);
         L.mmr = mm_plan_row((int)W);
-        L.fz = fused_plan(L.mmr, (int)W);
     }
     L.mixed = L.gen && !f64 && G == 1 && mixed_hw(d.H, d.W);
     L.ldw = (int)(N + 1);
     if (L.gen && !f64 && L.mm.ok && L.mmr.ok && env_int("ADMM_GEN_PITCH", 1)) L.ldw = (int)((N + 1 + 15) / 16 * 16);
     L.spec[0] = take(L.gen ? P * H * (size_t)L.ldw * csz : img);
     L.spec[1] = take(img);
-    // generic path: the r image (unfused step); the fused row pass's second spectrum (it reads its
-    // neighbours' halo rows, so it cannot write in place) shares the region
-    L.rimg = L.gen ? take(L.fz.ok ? std::max(img, P * H * (size_t)L.ldw * csz) : img) : 0;
+    // generic path: the r image (unfused step)
+    L.rimg = L.gen ? take(img) : 0;
     for (int i = 0; i < 4; ++i) L.u[i] = take(img);
     // b = H_t(xin), shared by the modules; on the fused path also without a PSF (b = xin re-laid
     // out for the inference pass, lane-paired rows)
@@ -1054,49 +1037,6 @@ MMPlan mm_plan_row(int W) {
     return m;
 }
 
-// the fused row pass (k_grow_fused_mm): the row inverse's decomposition; strips of up to 2 NLf rows (plus
-// two halo rows for the inverse), 512-thread blocks, one (line, k1) item per thread in the inverse's
-// first phase, at most 4 n-tiles per wave.  Off by default: measured slower than the step pass + the row
-// inverse (BSD 3,425-3,443 vs 4,371-4,372 it/s, profiles/r04_ab_fused_bsd.txt: the fused pass takes
-// 0.217 ms against 0.092 + 0.060 for the two kernels it replaces -- its ten barrier-separated phases leave
-// the CU waiting, SQ active share 0.23, profiles/r04_sq_bsd_mm.json).  A/B knobs: ADMM_GEN_FUSED=1,
-// ADMM_GEN_FUSED_NL (largest NLf, default 8)
-FusedPlan fused_plan(const MMPlan& row, int W) {
-    FusedPlan f{};
-    if (!row.ok || !env_int("ADMM_GEN_FUSED", 0)) return f;
-    f.S = row.S;
-    f.R = row.R;
-    f.h = row.h;
-    f.KS = row.KS;
-    f.MT = row.MT;
-    f.nth = 512;
-    const int G = (f.nth / 64) / f.MT, maxt = 4;
-    auto rp = [&](int nl) {
-        int r = std::max(4 * nl * f.S, 32 * ((nl * f.S + 7) / 8));
-        while (r % 64 != 32) r += 16;
-        return r;
-    };
-    auto tiles_ok = [&](int nl) { return G >= 1 && ((nl * f.S + 7) / 8 + G - 1) / G <= maxt; };
-    const int Wh = W / 2 + 1;
-    for (int nlf = std::max(1, std::min(8, env_int("ADMM_GEN_FUSED_NL", 8))); nlf >= 1; --nlf) {
-        const int nli = nlf + 1;
-        if (nli * (f.h + 1) > f.nth || !tiles_ok(nli) || !tiles_ok(nlf)) continue;
-        f.NLi = nli;
-        f.NLf = nlf;
-        f.RPi = rp(nli);
-        f.RPf = rp(nlf);
-        f.regA = std::max({2 * nli * Wh * 2, 4 * f.KS * f.RPi, 4 * f.KS * f.RPf});
-        f.regA = (f.regA + 3) / 4 * 4;
-        f.offX = f.regA;
-        f.offT = f.offX + (2 * nli * W + 3) / 4 * 4;  // x rows (nr + 2 <= 2 NLi), then the twiddles
-        f.lds = (size_t)(f.offT + 2 * W) * sizeof(float);
-        if (f.lds <= kMaxLds && 4 * nlf * Wh <= 2 * nli * W) {
-            f.ok = true;
-            return f;
-        }
-    }
-    return f;
-}
 
 // the launchers below are templated on the real type T of the solve: float, or double for fp64
 // inputs (ADMM_TV_FLAG_F64: the generic kernels' double instantiation, plans without Bluestein
@@ -1231,30 +1171,6 @@ int grow_inv(const cx_t<T>* spec, T* img, const cx_t<T>* tw, int W, long long ro
                            dim3(kF64<T> || GLB ? GNT : gen_threads("ADMM_GROW_NT")), lds, s, a);
         return launch_check("k_grow_inv");
     });
-}
-// the fused row pass of aniso inference (gfused_mm.hpp): spec_in -> (x, step, u) -> spec_out
-template <int S> int grow_fused_launch(const GFusedArgs& a, size_t lds, unsigned grid, hipStream_t s) {
-    if (int e = set_lds(k_grow_fused_mm<S>, lds)) return e;
-    hipLaunchKernelGGL(k_grow_fused_mm<S>, dim3(grid), dim3(512), lds, s, a);
-    return launch_check("k_grow_fused_mm");
-}
-int grow_fused(const FusedPlan& f, const cf* spec_in, cf* spec_out, const GStepArgs& g, const cf* tw, long long P, int H,
-               int W, int ld, hipStream_t s) {
-    if (P <= 0) return 0;
-    const int nstrip = (H + 2 * f.NLf - 1) / (2 * f.NLf);
-    const long long grid = P * nstrip;
-    if (grid > 0x7fffffffLL) return fail(ADMM_TV_EUNSUPPORTED, "too many row strips for the fused row pass");
-    GFusedArgs a{spec_in, spec_out, g.b, g.uxi, g.uyi, g.uxo, g.uyo, g.lam, g.rho, tw, P, H, W, W / 2 + 1, ld,
-                 f.R, f.h, f.KS, f.MT, f.NLi, f.RPi, f.NLf, f.RPf, nstrip, f.regA, f.offX, f.offT};
-    switch (f.S) {
-        case 1: return grow_fused_launch<1>(a, f.lds, (unsigned)grid, s);
-        case 2: return grow_fused_launch<2>(a, f.lds, (unsigned)grid, s);
-        case 3: return grow_fused_launch<3>(a, f.lds, (unsigned)grid, s);
-        case 4: return grow_fused_launch<4>(a, f.lds, (unsigned)grid, s);
-        case 5: return grow_fused_launch<5>(a, f.lds, (unsigned)grid, s);
-        case 8: return grow_fused_launch<8>(a, f.lds, (unsigned)grid, s);
-        default: return grow_fused_launch<13>(a, f.lds, (unsigned)grid, s);
-    }
 }
 
 template <int MODE, int BM, bool TWG, bool GLB, class T>
@@ -1464,33 +1380,6 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
         if (int e = grow_fwd(cb, cspec, twW, W, crows, st, gs, ld)) return e;  // r_1 = b
     }
     int uin = 0;
-    if constexpr (!kF64<T>) {
-        // aniso inference on the fused row pass: column pass in place, then row inverse + step + row
-        // forward in one kernel from one spectrum buffer into the other (gfused_mm.hpp)
-        if (!train && !d.iso && Lo.fz.ok) {
-            C* sa = cspec;
-            C* sb = at<C>(ws, Lo.rimg) + so;
-            for (int it = 1; it <= d.maxit; ++it) {
-                {
-                    ProfScope ps(1, st);
-                    if (int e = gcol<T>(sa, nullptr, fcT, mT, twH, H, W, np, 0, st, gs, Lo.mm, ld)) return e;
-                }
-                if (it == d.maxit) {
-                    ProfScope ps(1, st);
-                    return grow_inv<T>(sa, cout, twW, W, crows, st, gs, Lo.mmr, ld);
-                }
-                ProfScope ps(0, st);
-                const bool first = it == 1;
-                GStepArgs ga{nullptr, cb, first ? nullptr : u[2 * uin] + io, first ? nullptr : u[2 * uin + 1] + io,
-                             u[2 * (1 - uin)] + io, u[2 * (1 - uin) + 1] + io, nullptr, nullptr, nullptr, lam, rho,
-                             H, W, np * H * W};
-                if (int e = grow_fused(Lo.fz, sa, sb, ga, twW, np, H, W, ld, st)) return e;
-                std::swap(sa, sb);
-                uin = 1 - uin;
-            }
-            return 0;
-        }
-    }
     for (int it = 1; it <= d.maxit; ++it) {
         const bool last = it == d.maxit;
         {
@@ -1553,7 +1442,7 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     // Not under stream capture: a captured solve stays on the caller's stream.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cap));
-    const int ns = std::max(1, std::min(kMaxAux + 1, env_int("ADMM_GEN_STREAMS", 2)));
+    const int ns = std::max(1, std::min(kMaxAux + 1, env_setting("ADMM_GEN_STREAMS", 2)));
     const std::vector<long long> parts = gen_parts(P, H, ns);
     // (long lines: the parts would share the transform blocks' scratch slots -- one stream)
     const bool glb = make_plan(H, kF64<T>).glb || make_plan(W, kF64<T>).glb;
@@ -1581,24 +1470,32 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
     return solve_planes(0, P, s);
 }
 
-// rows per strip of the mixed row pass: a divisor of H (8, 4, 2 or 1), halved while there are fewer than
-// ~2 waves per SIMD of strips (the row group of a plan is Lg lanes: 16 ... 256)
 // rows per strip of the mixed row pass: the R dividing H that minimises (rounds of blocks over the chip)
 // x (R + 1) -- a strip of R rows inverts R + 1 row spectra (one halo row), and the blocks run in rounds
 // of (CUs x resident blocks per CU), so a short last round costs a whole one.  HD (1080 rows, 2 blocks of
 // 2 strips per CU): R = 15 -> 1,981 it/s against 1,910-1,927 with R = 8, and the model orders R = 8, 10,
 // 12, 15, 20, 24 as measured (profiles/r04_ab_hd_r.txt).  A/B knob ADMM_MIXED_R.
+// The block slots (CUs x resident pass A blocks) are queried once per (device, N) and cached.
+long long mixed_slots(int N) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<int, int>, long long>> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 512;
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto& c : cache)
+        if (c.first.first == dev && c.first.second == N) return c.second;
+    long long slots = 0;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+        slots = (long long)cus * std::max(1, admm_mixed::pass_a_blocks_per_cu(N));
+    if (slots <= 0) return 512;  // not cached: a failed query is retried
+    cache.push_back({{dev, N}, slots});
+    return slots;
+}
 int strip_rows_mixed(int H, long long rows, int N) {
     if (const int e = env_int("ADMM_MIXED_R", 0); e > 0 && H % e == 0) return e;
     const int sg = 256 / std::max(1, admm_mixed::row_lanes(N));  // strips per block
-    long long slots = 0;
-    {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ==
-                                                    hipSuccess)
-            slots = (long long)cus * std::max(1, admm_mixed::pass_a_blocks_per_cu(N));
-    }
-    if (slots <= 0) slots = 512;
+    const long long slots = mixed_slots(N);
     int best = 1;
     double best_t = 1e300;
     for (int R = 1; R <= 32 && R <= H; ++R) {

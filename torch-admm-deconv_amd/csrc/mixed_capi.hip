@@ -6,6 +6,7 @@
 #include <type_traits>
 
 #include "mixed_capi.hpp"
+#include "knobs.hpp"
 #include "mixed_kernels.hpp"
 
 using namespace admm;
@@ -173,10 +174,7 @@ hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long 
         constexpr int HH = decltype(h)::value;
         // plane groups of two at H >= 1024 (k_pass_b's measured tile order), plane-major below; A/B knob
         // ADMM_PASSB_M_ORDER (read once per process: it changes no sizes)
-        static const int forced = [] {
-            const char* e = std::getenv("ADMM_PASSB_M_ORDER");
-            return e ? std::atoi(e) : 0;
-        }();
+        static const int forced = env_int("ADMM_PASSB_M_ORDER", 0);
         const int order = forced > 0 ? forced : (HH >= 1024 ? 2 : 1);
         auto go = [&](auto cc) {
             constexpr int CC = decltype(cc)::value;

@@ -216,79 +216,6 @@ __device__ __forceinline__ void mfft(cf (&v)[EM], const Buf& buf, const cf* __re
     mrun<N, L, EM, 1, DIR, true, SYNC, TWMUL, Buf, Rs...>(v, buf, tw, t);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Ping-pong variant for transforms whose lanes span several waves (block barriers): consecutive LDS
-// exchanges alternate between two buffers, so an exchange is "write buf[ph]; barrier; read buf[ph];
-// ph ^= 1" -- one barrier instead of two (a write to a buffer is always separated by the barrier of
-// the exchange in between from the last reads of that buffer).  `ph` is the caller's exchange parity,
-// carried across transforms and other exchanges of the same lanes.
-// ---------------------------------------------------------------------------------------------
-// the two buffers are RowBuf{b0} and RowBuf{b0 + soff} (selected arithmetically: an indexed pair of
-// descriptors would be spilled to scratch)
-template <int N, int L, int EM, int R, int NS, int DIR, bool FIRST, bool LAST, int TWMUL>
-__device__ __forceinline__ void mstage_pp(cf (&v)[EM], cf* b0, int soff, int& ph, const cf* __restrict__ tw, int t) {
-    constexpr int NB = N / R;
-    constexpr int Q = (NB + L - 1) / L;
-    constexpr bool FULL = NB % L == 0;
-    static_assert(Q * R <= EM, "register array too small for this stage");
-    if constexpr (!FIRST) {
-        const RowBuf buf{b0 + (ph ? soff : 0)};
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int vt = t + L * q;
-            if (FULL || vt < NB) {
-#pragma unroll
-                for (int k = 0; k < R; ++k) v[q + Q * k] = buf.at(vt + k * NB);
-            }
-        }
-        ph ^= 1;
-    }
-    static_for<0, Q>([&](auto qc) {
-        constexpr int q = decltype(qc)::value;
-        const int vt = t + L * q;
-        if constexpr (NS > 1) {
-            const int m = vt % NS;
-#pragma unroll
-            for (int k = 1; k < R; ++k) {
-                const cf w = tw[(m * k) * (N / (NS * R)) * TWMUL];
-                v[q + Q * k] = DIR < 0 ? cmul(v[q + Q * k], w) : cmulc(v[q + Q * k], w);
-            }
-        }
-        cf y[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) y[k] = v[q + Q * k];
-        SDFT<R, DIR>::run(y);
-#pragma unroll
-        for (int k = 0; k < R; ++k) v[q + Q * k] = y[k];
-    });
-    if constexpr (!LAST) {
-        const RowBuf buf{b0 + (ph ? soff : 0)};
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int vt = t + L * q;
-            if (FULL || vt < NB) {
-                const int base = (vt / NS) * NS * R + vt % NS;
-#pragma unroll
-                for (int k = 0; k < R; ++k) buf.at(base + k * NS) = v[q + Q * k];
-            }
-        }
-        __syncthreads();
-    }
-}
-
-template <int N, int L, int EM, int NS, int DIR, bool FIRST, int TWMUL, int R, int... Rest>
-__device__ __forceinline__ void mrun_pp(cf (&v)[EM], cf* b0, int soff, int& ph, const cf* __restrict__ tw, int t) {
-    constexpr bool LAST = sizeof...(Rest) == 0;
-    mstage_pp<N, L, EM, R, NS, DIR, FIRST, LAST, TWMUL>(v, b0, soff, ph, tw, t);
-    if constexpr (!LAST) mrun_pp<N, L, EM, NS * R, DIR, false, TWMUL, Rest...>(v, b0, soff, ph, tw, t);
-}
-
-template <int N, int L, int EM, int DIR, int TWMUL, int... Rs>
-__device__ __forceinline__ void mfft_pp(cf (&v)[EM], cf* b0, int soff, int& ph, const cf* __restrict__ tw, int t,
-                                        Sched<Rs...>) {
-    mrun_pp<N, L, EM, 1, DIR, true, TWMUL, Rs...>(v, b0, soff, ph, tw, t);
-}
-
 // registers a schedule needs: max over its stages of R ceil(N / (R L))
 template <int N, int L> __host__ __device__ constexpr int stage_regs(int R) { return R * ((N / R + L - 1) / L); }
 template <int N, int L, int... Rs> __host__ __device__ constexpr int sched_regs(Sched<Rs...>) {

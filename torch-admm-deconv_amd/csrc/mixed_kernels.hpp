@@ -55,27 +55,12 @@ template <> struct MRow<1024> {  // W = 2048 beside a smooth H: 128 lanes x 8 (2
 // smooth rows.  Rows whose pixel state would exceed ~8 pairs per lane at 64 lanes run "wide": a row
 // group of 128 or 256 lanes (2 or 4 waves of the block) exchanging through LDS with block barriers, so
 // each lane keeps 8 pixel pairs (15 per lane at 64 lanes measured ~320 VGPRs: 1 wave per SIMD).
-// ADMM_M960_V (A/B build knob): 0 = 960 as 8 * 15 * 8, 1 = 8 * 3 * 5 * 8 (smaller butterflies, one more
-// exchange)
-#ifndef ADMM_M960_V
-#define ADMM_M960_V 0
-#endif
+// (measured slower for 960: 8 * 3 * 5 * 8, pass A 0.304 -> 0.327 ms, profiles/r04_ab_hd_m960v1.txt; 4-wave
+// groups of 4 pairs per lane as 4 * 15 * 4 * 4)
 template <> struct MRow<960> {  // W = 1920 (HD): 960 = 8 * 15 * 8 over 120 of 128 lanes
-#if ADMM_M960_V == 2  // 4-wave row groups, 4 pixel pairs per lane: 4 * 15 * 4 * 4 over 240 of 256 lanes
-    static constexpr int Lg = 256, Lp = 240, Ep = 4, Ls = 240, Es = 4;
-    using Inv = Sched<4, 15, 4, 4>;
-    using Fwd = Sched<4, 4, 15, 4>;
-#else
     static constexpr int Lg = 128, Lp = 120, Ep = 8, Ls = 120, Es = 8;
-#endif
-#if ADMM_M960_V == 1
-    using Inv = Sched<8, 3, 5, 8>;
-    using Fwd = Sched<8, 5, 3, 8>;
-#elif ADMM_M960_V == 2
-#else
     using Inv = Sched<8, 15, 8>;
     using Fwd = Sched<8, 15, 8>;
-#endif
 };
 template <> struct MRow<1920> {  // W = 3840 (4K UHD): spectra and pixels 240 x 8 (4 waves), 8 * 6 * 5 * 8
     static constexpr int Lg = 256, Lp = 240, Ep = 8, Ls = 240, Es = 8;
@@ -87,42 +72,24 @@ template <> struct MRow<2048> {  // W = 4096: 256 lanes x 8 (4 waves)
     using Inv = Sched<8, 4, 8, 8>;
     using Fwd = Sched<8, 8, 4, 8>;
 };
-// ADMM_MROW_V (A/B build knob): 1 = 720p / VGA row schedules with fewer values per stage (640: 10 * 8 * 8
-// over 64 / 80 lanes, 320: 8 * 5 * 8 over 40 lanes)
-#ifndef ADMM_MROW_V  // 1: VGA pass A 0.201 -> 0.182 ms, 720p 0.333 -> 0.326 (profiles/r04_ab_vga_rows.txt, r04_ab_p720_rows.txt)
-#define ADMM_MROW_V 1
-#endif
-#if ADMM_MROW_V == 1
+// 720p / VGA rows with fewer values per stage (640: 10 * 8 * 8 over 64 / 80 lanes, 320: 8 * 5 * 8 over 40
+// lanes) than 5 * 16 * 8 / 16 * 4 * 5: VGA pass A 0.201 -> 0.182 ms, 720p 0.333 -> 0.326
+// (profiles/r04_ab_vga_rows.txt, r04_ab_p720_rows.txt)
 template <> struct MRow<640> {  // W = 1280 (720p): spectra 64 x 10, pixels 80 x 8 (2 waves)
     static constexpr int Lg = 128, Lp = 80, Ep = 8, Ls = 64, Es = 10;
     using Inv = Sched<10, 8, 8>;
     using Fwd = Sched<8, 8, 10>;
 };
-#else
-template <> struct MRow<640> {  // W = 1280 (720p): spectra 128 x 5, pixels 80 x 8 (2 waves)
-    static constexpr int Lg = 128, Lp = 80, Ep = 8, Ls = 128, Es = 5;
-    using Inv = Sched<5, 16, 8>;
-    using Fwd = Sched<8, 16, 5>;
-};
-#endif
 template <> struct MRow<480> {  // W = 960: spectra 40 x 12, pixels 60 x 8
     static constexpr int Lg = 64, Lp = 60, Ep = 8, Ls = 40, Es = 12;
     using Inv = Sched<12, 5, 8>;
     using Fwd = Sched<8, 5, 12>;
 };
-#if ADMM_MROW_V == 1
 template <> struct MRow<320> {  // W = 640 (VGA): spectra 40 x 8, pixels 40 x 8
     static constexpr int Lg = 64, Lp = 40, Ep = 8, Ls = 40, Es = 8;
     using Inv = Sched<8, 5, 8>;
     using Fwd = Sched<8, 5, 8>;
 };
-#else
-template <> struct MRow<320> {  // W = 640 (VGA): spectra 20 x 16, pixels 64 x 5
-    static constexpr int Lg = 64, Lp = 64, Ep = 5, Ls = 20, Es = 16;
-    using Inv = Sched<16, 4, 5>;
-    using Fwd = Sched<5, 4, 16>;
-};
-#endif
 template <> struct MRow<240> {  // W = 480: spectra 16 x 15, pixels 30 x 8
     static constexpr int Lg = 32, Lp = 30, Ep = 8, Ls = 16, Es = 15;
     using Inv = Sched<15, 2, 8>;
@@ -160,9 +127,6 @@ template <> struct MRow<1280> {  // W = 2560: spectra 160 x 8, pixels 256 x 5 (4
     using Fwd = Sched<5, 8, 4, 8>;
 };
 
-#ifndef ADMM_MIXED_PP
-#define ADMM_MIXED_PP 0
-#endif
 template <int N> struct MRowG {
     using P = MRow<N>;
     static constexpr int Lg = P::Lg, Lp = P::Lp, Ep = P::Ep, Ls = P::Ls, Es = P::Es, W = 2 * N;
@@ -180,11 +144,8 @@ template <int N> struct MRowG {
                   "inverse edges");
     static_assert(edge_ok<N, Lg>(sched_first(typename P::Fwd{}), Lp) && edge_ok<N, Lg>(sched_last(typename P::Fwd{}), Ls),
                   "forward edges");
-    // ADMM_MIXED_PP (A/B build knob): wide row groups ping-pong between two exchange buffers (one barrier
-    // per exchange) instead of one buffer with a barrier before and after each write
-    static constexpr bool PP = WIDE && ADMM_MIXED_PP != 0;
-    static constexpr int NBUF = PP ? 2 : 1;
-    static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * NBUF * RowBuf::slots(N)); }
+    // one exchange buffer per sub-group (ping-pong buffers for the wide groups measured within +-0.5 %)
+    static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * RowBuf::slots(N)); }
 };
 
 template <int H> struct MCol;
@@ -204,51 +165,26 @@ template <> struct MCol<1024> : MColPow2<1024> {};
 template <> struct MCol<2048> : MColPow2<2048> {};
 template <> struct MCol<4096> : MColPow2<4096> {};
 // columns per block of the smooth column plans: 8 (64-byte row segments, pairs of blocks sharing each
-// 128-byte line, as k_pass_b) wherever 8 Lc <= 1024 threads; ADMM_MCOL_C (A/B build knob) overrides
-#ifndef ADMM_MCOL_C
-#define ADMM_MCOL_C 8
-#endif
-// ADMM_M1080_V (A/B build knob): 0 = 120 threads x 9 values per column (960-thread blocks: one block per
-// CU at 112 VGPRs), 1 = 60 threads x 18 values (480-thread blocks: two per CU, twice the bytes in flight),
-// 2 = the 120 x 9 layout with the 9 * 12 * 10 schedule
-#ifndef ADMM_M1080_V  // 2: HD pass B 0.160 -> 0.120 ms, 62 VGPRs (profiles/r04_ab_hd_m1080s.txt)
-#define ADMM_M1080_V 2
-#endif
+// 128-byte line, as k_pass_b) wherever 8 Lc <= 1024 threads
+// 1080: 120 threads x 9 values per column, schedule 9 * 12 * 10 -- lanes busy 100 / 75 / 90 % per stage
+// (9 * 15 * 8: 100 / 60 / 56 %), 12 values: HD pass B 0.160 -> 0.120 ms, 62 VGPRs
+// (profiles/r04_ab_hd_m1080s.txt; 60 threads x 18 values measured 6 % slower)
 template <> struct MCol<1080> {
-#if ADMM_M1080_V == 1
-    static constexpr int Lc = 60, Ec = 18, C = ADMM_MCOL_C;
-#else
-    static constexpr int Lc = 120, Ec = 9, C = ADMM_MCOL_C;
-#endif
-#if ADMM_M1080_V == 2  // 9 * 12 * 10: lanes busy 100 / 75 / 90 % per stage (9 * 15 * 8: 100 / 60 / 56 %), 12 values
+    static constexpr int Lc = 120, Ec = 9, C = 8;
     using Fwd = Sched<9, 12, 10>;
     using Inv = Sched<10, 12, 9>;
-#else
-    using Fwd = Sched<9, 15, 8>;
-    using Inv = Sched<8, 15, 9>;
-#endif
 };
-// ADMM_M2160_V / ADMM_M360_V (A/B build knobs): 1 = schedules that keep more lanes busy per guarded stage
-// (2160: 9 * 2 * 12 * 10, lanes 100 / 90 / 75 / 90 %, 12 values, one more exchange, vs 9 * 16 * 15 at
-// 100 / 56 / 60 %, 16 values; 360: 9 * 10 * 4 vs 9 * 8 * 5)
-#ifndef ADMM_M2160_V  // 1: 4K UHD pass B 0.2345 -> 0.214 ms (profiles/r04_ab_uhd_cols.txt)
-#define ADMM_M2160_V 1
-#endif
-#ifndef ADMM_M360_V  // 1: 360x720 pass B 0.0566 -> 0.0545 ms (profiles/r04_ab_sd_cols.txt)
-#define ADMM_M360_V 1
-#endif
+// schedules that keep more lanes busy per guarded stage: 2160 as 9 * 2 * 12 * 10 (lanes 100 / 90 / 75 /
+// 90 %, 12 values, one more exchange) instead of 9 * 16 * 15 (100 / 56 / 60 %, 16 values): 4K UHD pass B
+// 0.2345 -> 0.214 ms (profiles/r04_ab_uhd_cols.txt); 360 as 9 * 10 * 4 instead of 9 * 8 * 5: 0.0566 ->
+// 0.0545 ms (profiles/r04_ab_sd_cols.txt)
 template <> struct MCol<2160> {
     static constexpr int Lc = 240, Ec = 9, C = 2;
-#if ADMM_M2160_V == 1
     using Fwd = Sched<9, 2, 12, 10>;
     using Inv = Sched<10, 12, 2, 9>;
-#else
-    using Fwd = Sched<9, 16, 15>;
-    using Inv = Sched<15, 16, 9>;
-#endif
 };
 template <> struct MCol<720> {
-    static constexpr int Lc = 80, Ec = 9, C = ADMM_MCOL_C;
+    static constexpr int Lc = 80, Ec = 9, C = 8;
     using Fwd = Sched<9, 16, 5>;
     using Inv = Sched<5, 16, 9>;
 };
@@ -258,7 +194,7 @@ template <> struct MCol<960> {
     using Inv = Sched<4, 16, 15>;
 };
 template <> struct MCol<540> {
-    static constexpr int Lc = 60, Ec = 9, C = ADMM_MCOL_C;
+    static constexpr int Lc = 60, Ec = 9, C = 8;
     using Fwd = Sched<9, 12, 5>;
     using Inv = Sched<5, 12, 9>;
 };
@@ -269,13 +205,8 @@ template <> struct MCol<480> {
 };
 template <> struct MCol<360> {
     static constexpr int Lc = 40, Ec = 9, C = 8;
-#if ADMM_M360_V == 1
     using Fwd = Sched<9, 10, 4>;
     using Inv = Sched<4, 10, 9>;
-#else
-    using Fwd = Sched<9, 8, 5>;
-    using Inv = Sched<5, 8, 9>;
-#endif
 };
 template <> struct MCol<240> {
     static constexpr int Lc = 16, Ec = 15, C = 8;
@@ -355,19 +286,17 @@ template <int N> struct RowXfM {
             return mkc(sm.x + d.y, sm.y - d.x);
         }
     }
-    // the row group's LDS: one exchange buffer (a single wave), or two used in turn with the exchange
-    // parity ph (wide groups: one barrier per exchange, mixed_fft.hpp mstage_pp)
+    // the row group's LDS exchange buffer
     struct Lds {
-        cf* base;  // buffer 0; buffer 1 (wide groups) RowBuf::slots(N) further
-        int ph;
-        __device__ __forceinline__ RowBuf cur() const { return RowBuf{base + (ph ? RowBuf::slots(N) : 0)}; }
+        cf* base;
+        __device__ __forceinline__ RowBuf cur() const { return RowBuf{base}; }
     };
-    __device__ __forceinline__ static Lds lds_of(cf* base) { return Lds{base, 0}; }
+    __device__ __forceinline__ static Lds lds_of(cf* base) { return Lds{base}; }
     // wide row groups: the partners through the LDS exchange buffer (every lane of the block takes part)
     template <bool INV>
     __device__ __forceinline__ static void combine_lds(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
         const RowBuf buf = l.cur();
-        if (!G::PP) lds_barrier();  // one buffer: its previous readers are done
+        lds_barrier();  // its previous readers are done
         if (t < Ls) {
 #pragma unroll
             for (int j = 0; j < Es; ++j) buf.at(t + Ls * j) = v[j];
@@ -384,7 +313,6 @@ template <int N> struct RowXfM {
                 v[j] = one<INV>(k, x, buf.at(kp >= 0 ? kp : 0), tw);
             }
         }
-        if (G::PP) l.ph ^= 1;
     }
     // The Hermitian combine of element k = t + Ls j with its partner N - k, which sits in lane
     // Ls - t, register Es - 1 - j (t = 0: this lane, register Es - j).  Registers j and Es - 1 - j are
@@ -418,10 +346,7 @@ template <int N> struct RowXfM {
     }
     // row spectrum in layout(Es) (v[j], j < Es) -> pixel pairs in layout(Ep) (v[j], j < Ep), x 2W
     __device__ __forceinline__ static void c2r(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
-        if constexpr (G::PP) {
-            combine_lds<true>(v, l, tw, t);
-            mfft_pp<N, Lg, EM, +1, 2>(v, l.base, RowBuf::slots(N), l.ph, tw, t, typename MRow<N>::Inv{});
-        } else if constexpr (WIDE) {
+        if constexpr (WIDE) {
             combine_lds<true>(v, l, tw, t);
             mfft<N, Lg, EM, +1, SYNC, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Inv{});
         } else {
@@ -431,10 +356,7 @@ template <int N> struct RowXfM {
     }
     // pixel pairs in layout(Ep) -> packed spectrum (2 rfft) in layout(Es)
     __device__ __forceinline__ static void r2c(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
-        if constexpr (G::PP) {
-            mfft_pp<N, Lg, EM, -1, 2>(v, l.base, RowBuf::slots(N), l.ph, tw, t, typename MRow<N>::Fwd{});
-            combine_lds<false>(v, l, tw, t);
-        } else if constexpr (WIDE) {
+        if constexpr (WIDE) {
             mfft<N, Lg, EM, -1, SYNC, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Fwd{});
             combine_lds<false>(v, l, tw, t);
         } else {
@@ -448,7 +370,7 @@ template <int N> struct RowXfM {
     __device__ __forceinline__ static void neighbour(const float (&val)[Ep], float (&out)[Ep], Lds& l, int t) {
         if constexpr (WIDE) {
             const RowBuf buf = l.cur();
-            if (!G::PP) lds_barrier();
+            lds_barrier();
             if (t < Lp) {
 #pragma unroll
                 for (int j = 0; j < Ep; ++j) buf.at(t + Lp * j).x = val[j];
@@ -460,7 +382,6 @@ template <int N> struct RowXfM {
                 k = k < 0 ? N - 1 : k >= N ? 0 : k;
                 out[j] = buf.at(k).x;
             }
-            if (G::PP) l.ph ^= 1;
         } else {
             const int src = SHIFT < 0 ? (t == 0 ? Lp - 1 : t - 1) : (t + 1 >= Lp ? 0 : t + 1);
             float sh[Ep];
@@ -490,7 +411,7 @@ __global__ void __launch_bounds__(256) k_row_r2c_m(const float* __restrict__ img
     const bool ok = row < rows;
     if (!G::WIDE && !ok) return;  // (a wide row group keeps every lane for the block barriers)
     if (!ok) row = rows - 1;
-    auto lx = RowXfM<N>::lds_of(tw + G::W + sgl * G::NBUF * RowBuf::slots(N));
+    auto lx = RowXfM<N>::lds_of(tw + G::W + sgl * RowBuf::slots(N));
     const cf* src = reinterpret_cast<const cf*>(img + row * G::W);
     cf v[EM];
     if (t < Lp) {
@@ -520,7 +441,7 @@ __global__ void __launch_bounds__(256) k_row_c2r_m(const cf* __restrict__ spec, 
     const bool ok = row < rows;
     if (!G::WIDE && !ok) return;
     if (!ok) row = rows - 1;
-    auto lx = RowXfM<N>::lds_of(tw + G::W + sgl * G::NBUF * RowBuf::slots(N));
+    auto lx = RowXfM<N>::lds_of(tw + G::W + sgl * RowBuf::slots(N));
     const cf* src = spec + row * N;
     cf v[EM];
     if (t < Ls) {
@@ -549,23 +470,13 @@ static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restri
 // ---------------------------------------------------------------------------------------------
 // pass B: column FFT -> Wiener factor -> column IFFT, in place, C columns per block
 // ---------------------------------------------------------------------------------------------
-// ADMM_PASSB_M_WPE (A/B build knob): an occupancy target (waves per SIMD) for the smooth column plans, so
-// more blocks fit per CU (0: the compiler's choice)
-#ifndef ADMM_PASSB_M_WPE
-#define ADMM_PASSB_M_WPE 0
-#endif
-#ifndef ADMM_PASSB_M_LATEF  // 1: HD pass B 0.183 -> 0.160 ms, 1,790 -> 1,910 it/s (profiles/r04_ab_hd_latef.txt)
-#define ADMM_PASSB_M_LATEF 1
-#endif
 // Measured and not kept (profiles/r04_ab_hd_passb_gp.txt): blocks walking 2-8 planes of their column
 // block with the next plane streamed into LDS (global_load_lds) during the inverse transform and
-// LDS-only barriers -- HD pass B 0.258-0.267 ms against 0.160 for one tile per block.
-template <int H> constexpr int passb_m_wpe() { return (H & (H - 1)) == 0 ? 0 : ADMM_PASSB_M_WPE; }
+// LDS-only barriers -- HD pass B 0.258-0.267 ms against 0.160 for one tile per block; an occupancy
+// target for the smooth column plans (capped registers spill and lose 4-21 %).
 template <int H, int CC>
-__global__ void __launch_bounds__((MColG<H, CC>::NT)) __attribute__((amdgpu_waves_per_eu(passb_m_wpe<H>(), 0)))
-k_pass_b_m(cf* spec, const float* __restrict__ fcM,
-                                                           const cf* __restrict__ twH_g, int N, int colblocks,
-                                                           int order) {
+__global__ void __launch_bounds__((MColG<H, CC>::NT))
+k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g, int N, int colblocks, int order) {
     using G = MColG<H, CC>;
     constexpr int Lc = G::Lc, Ec = G::Ec, C = G::C, EM = G::EM, NBz = G::NBz, Qz = G::Qz;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -595,12 +506,11 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM,
                 m[q + Qz * k] = (vt < NBz) ? fcM[(size_t)(vt + NBz * k) * (N + 1) + col] : 0.f;
         }
     };
-    // ADMM_PASSB_M_LATEF (A/B build knob): load the factors after the forward transform (fewer live
-    // registers through it) instead of issuing them with the data
-    if constexpr (!ADMM_PASSB_M_LATEF) load_m();
     __syncthreads();  // twiddles in LDS
     mfft<H, Lc, EM, -1, 1, 1>(v, buf, tw, t, typename MCol<H>::Fwd{});
-    if constexpr (ADMM_PASSB_M_LATEF) load_m();
+    // the factors are loaded after the forward transform (fewer live registers through it) rather than
+    // with the data: HD pass B 0.183 -> 0.160 ms (profiles/r04_ab_hd_latef.txt)
+    load_m();
     if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H - ky]
         __syncthreads();
 #pragma unroll
@@ -645,13 +555,7 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM,
 // ---------------------------------------------------------------------------------------------
 // occupancy target of the mixed row pass (waves per SIMD): the plans keep <= 9 pixel pairs per lane
 // (wide row groups where a wave would need more), ~150-170 VGPRs: 2 guaranteed, 3 when they fit
-#ifndef PASSA_M_MINW
-#ifdef ADMM_PASSA_M_W  // A/B build knob: one occupancy target for every row plan
-#define PASSA_M_MINW(ep) (ADMM_PASSA_M_W)
-#else
 #define PASSA_M_MINW(ep) ((ep) > 9 ? 1 : 2)
-#endif
-#endif
 template <int N, bool ISO, bool FIRST>
 __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(PassAArgs a) {
     using G = MRowG<N>;
@@ -671,7 +575,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
     const int spp = H / R;
     const long long p = strip / spp;
     const int i0 = (int)(strip % spp) * R;
-    auto lx = RowXfM<N>::lds_of(tw + W + sgl * G::NBUF * RowBuf::slots(N));
+    auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
     const float rho = a.rho[0];
     const float tau = a.lam[0] / rho;
     const bool pa = t < Lp, sa = t < Ls;  // lane holds pixels / spectrum elements
@@ -810,7 +714,7 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
     const int g = (int)(item % H);
     const int grp = (int)(item / H);
     const int gm = g == 0 ? H - 1 : g - 1;
-    auto lx = RowXfM<N>::lds_of(tw + W + sgl * G::NBUF * RowBuf::slots(N));
+    auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
     const bool pa = t < Lp, sa = t < Ls;
     cf sx[Ep], sy[Ep];
 #pragma unroll
