@@ -205,7 +205,10 @@ def test_environment_reads_are_gated():
     assert re.search(r"inline int env_int\(const char\* name, int dflt\) \{ return ADMM_AB_BUILD \?", knobs_hpp)
     assert re.search(r"#ifndef ADMM_AB_BUILD\s*#define ADMM_AB_BUILD 0", knobs_hpp)
     mk = open(os.path.join(CSRC, "Makefile")).read()
-    assert "ADMM_AB_BUILD" not in mk  # the release build never turns the knobs on
+    # the release library's flags never turn the knobs on; only the separate A/B target does
+    rules = "\n".join(ln for ln in mk.splitlines() if not ln.lstrip().startswith("#"))
+    assert re.search(r"^EXTRA\s*\?=\s*$", mk, re.M) and rules.count("ADMM_AB_BUILD=1") == 1
+    assert re.search(r"^ab:\n\t\$\(MAKE\) OBJDIR=build_ab OUT=\$\(AB_OUT\) EXTRA=-DADMM_AB_BUILD=1", mk, re.M)
     assert all(s in knobs_hpp for s in RUNTIME_SETTINGS)
     integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert all(s in integ for s in RUNTIME_SETTINGS)
@@ -226,3 +229,8 @@ def test_release_library_ignores_ab_knobs():
     outs = [subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, check=True).stdout
             for e in (env0, env1)]
     assert outs[0] == outs[1] and len(outs[0].split()) == 6
+    # ... while the A/B build (admmtor._native.ab_library: tests comparing kernel paths) follows them
+    code_ab = code.replace("from admmtor import _native\n", "from admmtor import _native\n_native._lib = _native._open(_native.AB_LIB_PATH)\n")
+    ab = [subprocess.run([sys.executable, "-c", code_ab], env=e, capture_output=True, text=True, check=True).stdout
+          for e in (env0, env1)]
+    assert ab[0] == outs[0] and ab[1] != ab[0]

@@ -164,16 +164,21 @@ def test_shift_equivariance(cuda_dev):
 def test_iso_plane_grouping_invariance(cuda_dev, monkeypatch):
     """iso: the per-pixel norm over (B, C) does not depend on how the norm pass groups planes
     (1, 5, 64 planes per group or the library's rule) beyond fp32 reassociation, and every
-    grouping stays within the gate of the fp64 oracle."""
+    grouping stays within the gate of the fp64 oracle.  The groupings are A/B knobs: the release
+    library (the rule) and the A/B build (ADMM_ISO_PPG) run them."""
+    from admmtor import _native
     from admmtor.synth import blurred_batch, make_psf
     k = make_psf("gauss:2", 9)
     x = blurred_batch(4, 3, 128, 128, k, seed=5)
     ref = oracle(x, k, 0.01, 0.02, True, 10)
-    outs = []
+    outs = [solve(x, k, 0.01, 0.02, True, 10, cuda_dev)]
+    assert rel(outs[0], ref) <= 1e-5
     for ppg in ("0", "1", "5", "64"):
         monkeypatch.setenv("ADMM_ISO_PPG", ppg)
-        outs.append(solve(x, k, 0.01, 0.02, True, 10, cuda_dev))
+        with _native.ab_library():
+            outs.append(solve(x, k, 0.01, 0.02, True, 10, cuda_dev))
         assert rel(outs[-1], ref) <= 1e-5, ppg
+    assert torch.equal(outs[0], outs[1])  # the A/B build at its defaults is the release library
     # reassociated fp32 sums pass through the block-shrink's threshold every iteration: the
     # groupings differ at the fp32 noise floor (3e-6 measured), not beyond the gate
     for o in outs[1:]:

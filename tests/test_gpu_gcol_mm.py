@@ -11,6 +11,7 @@ both meet the gate and agree to ~1e-6.
 import pytest
 import torch
 
+from admmtor import _native
 from test_gpu_generic import TOL_REF64, oracle, rel, solve
 
 pytestmark = pytest.mark.gpu
@@ -46,7 +47,8 @@ def test_mm_column_pass_vs_oracle(cuda_dev, shape, psf, iso, monkeypatch):
     ref = oracle(x, k, 0.01, 0.02, iso, it)
     got = solve(x, k, 0.01, 0.02, iso, it, cuda_dev)
     monkeypatch.setenv("ADMM_GCOL_MM", "0")
-    lds = solve(x, k, 0.01, 0.02, iso, it, cuda_dev)
+    with _native.ab_library():  # the LDS pass: an A/B knob
+        lds = solve(x, k, 0.01, 0.02, iso, it, cuda_dev)
     e, e_lds, d = rel(got, ref), rel(lds, ref), rel(got, lds)
     print(shape, psf, "iso" if iso else "aniso", f"matrix-core {e:.3e}  LDS pass {e_lds:.3e}  between {d:.3e}")
     assert e <= TOL_REF64
@@ -76,7 +78,8 @@ def test_mm_row_inverse_vs_oracle(cuda_dev, shape, psf, iso, monkeypatch):
     ref = oracle(x, k, 0.01, 0.02, iso, 15)
     got = solve(x, k, 0.01, 0.02, iso, 15, cuda_dev)
     monkeypatch.setenv("ADMM_GROW_MM", "0")
-    lds = solve(x, k, 0.01, 0.02, iso, 15, cuda_dev)
+    with _native.ab_library():
+        lds = solve(x, k, 0.01, 0.02, iso, 15, cuda_dev)
     e, e_lds = rel(got, ref), rel(lds, ref)
     print(shape, psf, "iso" if iso else "aniso", f"matrix-core rows {e:.3e}  LDS rows {e_lds:.3e}")
     assert e <= TOL_REF64

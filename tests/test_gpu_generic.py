@@ -102,10 +102,14 @@ def test_bluestein_matches_direct_prime_stages(cuda_dev, shape, monkeypatch):
     k = make_psf("gauss:1.5", 9)
     x = blurred_batch(*shape, k, seed=7)
     ref = oracle(x, k, 0.01, 0.02, False, 15)
-    monkeypatch.setenv("ADMM_BLUE_MIN", "0")
-    e_direct = rel(solve(x, k, 0.01, 0.02, False, 15, cuda_dev), ref)
-    monkeypatch.setenv("ADMM_BLUE_MIN", "11")
-    e_blue = rel(solve(x, k, 0.01, 0.02, False, 15, cuda_dev), ref)
+    from admmtor import _native
+    e_blue0 = rel(solve(x, k, 0.01, 0.02, False, 15, cuda_dev), ref)  # the release library's plan
+    with _native.ab_library():  # the Bluestein threshold is an A/B knob
+        monkeypatch.setenv("ADMM_BLUE_MIN", "0")
+        e_direct = rel(solve(x, k, 0.01, 0.02, False, 15, cuda_dev), ref)
+        monkeypatch.setenv("ADMM_BLUE_MIN", "11")
+        e_blue = rel(solve(x, k, 0.01, 0.02, False, 15, cuda_dev), ref)
+    assert e_blue0 <= TOL_REF64
     print(shape, f"vs fp64 oracle: bluestein {e_blue:.3e}, direct {e_direct:.3e}")
     assert e_blue <= TOL_REF64
     assert e_blue <= 2 * e_direct + 1e-6
@@ -118,10 +122,11 @@ def test_fused_step_is_bit_identical(cuda_dev, shape, iso, monkeypatch):
     from admmtor.synth import blurred_batch, make_psf
     k = make_psf("gauss:1.5", 5)
     x = blurred_batch(*shape, k, seed=3)
+    from admmtor import _native
     monkeypatch.setenv("ADMM_GSTEP_FUSE", "0")
-    a = solve(x, k, 0.01, 0.02, iso, 12, cuda_dev)
-    monkeypatch.setenv("ADMM_GSTEP_FUSE", "1")
-    b = solve(x, k, 0.01, 0.02, iso, 12, cuda_dev)
+    with _native.ab_library():  # the separate kernels: an A/B knob
+        a = solve(x, k, 0.01, 0.02, iso, 12, cuda_dev)
+    b = solve(x, k, 0.01, 0.02, iso, 12, cuda_dev)  # the release library: fused
     assert torch.equal(a, b)
 
 

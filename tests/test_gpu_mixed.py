@@ -77,8 +77,9 @@ def test_mixed_vs_oracle_and_generic(cuda_dev, monkeypatch, shape, psf, iso, it)
     x = blurred_batch(*shape, k if k is not None else torch.empty(0), seed=sum(shape) + it)
     got = solve(x, k, iso, it, cuda_dev)
     ref = oracle(x, k, iso, it)
-    monkeypatch.setenv("ADMM_MIXED", "0")  # the same solve on the generic kernels
-    gen = solve(x, k, iso, it, cuda_dev)
+    monkeypatch.setenv("ADMM_MIXED", "0")  # the same solve on the generic kernels (an A/B knob)
+    with _native.ab_library():
+        gen = solve(x, k, iso, it, cuda_dev)
     e_ref, e_gen, e_gen_ref = rel(got, ref), rel(got, gen), rel(gen, ref)
     print(shape, psf, "iso" if iso else "aniso", it, f"mixed vs fp64 oracle {e_ref:.2e}, vs generic {e_gen:.2e} "
           f"(generic vs oracle {e_gen_ref:.2e})")

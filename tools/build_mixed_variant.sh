@@ -11,5 +11,5 @@ rm -rf $C/build_$NAME && mkdir -p $C/build_$NAME tools/_variants
 cp -p $C/build/*.o $C/build/build_hash.cpp $C/build_$NAME/
 rm -f $C/build_$NAME/mixed_capi.o
 make -C $C -j8 OBJDIR=build_$NAME OUT=../../tools/_variants/$NAME.so \
-  CXXFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -I../../include -ffp-contract=off -fno-slp-vectorize -DADMM_AB_BUILD=1 $*" >/dev/null
+  CXXFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -I../../include -ffp-contract=off -fno-slp-vectorize -DADMM_AB_BUILD=1 $*" ../../tools/_variants/$NAME.so >/dev/null
 echo built tools/_variants/$NAME.so

@@ -7,5 +7,5 @@ cd "$(dirname "$0")/.."
 NAME=$1; shift
 mkdir -p tools/_variants
 make -C torch-admm-deconv_amd/csrc -j8 OBJDIR=build_$NAME OUT=../../tools/_variants/$NAME.so \
-  CXXFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -I../../include -ffp-contract=off -fno-slp-vectorize -DADMM_AB_BUILD=1 $*" >/dev/null
+  CXXFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -I../../include -ffp-contract=off -fno-slp-vectorize -DADMM_AB_BUILD=1 $*" ../../tools/_variants/$NAME.so >/dev/null
 echo built tools/_variants/$NAME.so

@@ -5,6 +5,7 @@ library is missing or fails to load, every entry point raises loudly.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import glob
 import hashlib
@@ -13,6 +14,9 @@ import threading
 
 _LIB_PATH = os.environ.get("ADMMTOR_LIB_OVERRIDE") or \
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libadmm_tv.so")  # override: tuning A/B only
+# the same sources built with -DADMM_AB_BUILD=1 (csrc/knobs.hpp): its A/B knobs follow the environment.
+# Never used by the package itself; tests that compare alternative kernels select it with ab_library().
+AB_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libadmm_tv_ab.so")
 
 ADMM_TV_OK = 0
 ADMM_TV_EINVAL = -1
@@ -120,70 +124,95 @@ def load() -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(_LIB_PATH):
-            raise ImportError(
-                f"admmtor: the HIP library {_LIB_PATH} is missing. Build it with "
-                "`python __graft_entry__.py build` (or `make -C torch-admm-deconv_amd/csrc`). "
-                "There is no CPU fallback.")
-        L = ctypes.CDLL(_LIB_PATH)
-        vp, sz = ctypes.c_void_p, ctypes.c_size_t
-        dp = ctypes.POINTER(AdmmTvDesc)
-        L.admm_tv_abi_version.restype = ctypes.c_int
-        L.admm_tv_abi_version.argtypes = []
-        L.admm_tv_build_hash.restype = ctypes.c_char_p
-        L.admm_tv_build_hash.argtypes = []
-        L.admm_tv_supported.restype = ctypes.c_int
-        L.admm_tv_supported.argtypes = [ctypes.c_int64, ctypes.c_int64]
-        L.admm_tv_supported_f64.restype = ctypes.c_int
-        L.admm_tv_supported_f64.argtypes = [ctypes.c_int64, ctypes.c_int64]
-        L.admm_tv_workspace_size.restype = ctypes.c_int
-        L.admm_tv_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
-        for f in ("admm_tv_forward", "admm_tv_forward_f64"):
-            getattr(L, f).restype = ctypes.c_int
-            getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp]
-        L.admm_tv_history_size.restype = ctypes.c_int
-        L.admm_tv_history_size.argtypes = [dp, ctypes.POINTER(sz)]
-        for f in ("admm_tv_forward_train", "admm_tv_forward_train_f64"):
-            getattr(L, f).restype = ctypes.c_int
-            getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp]
-        L.admm_tv_backward_workspace_size.restype = ctypes.c_int
-        L.admm_tv_backward_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
-        for f in ("admm_tv_backward", "admm_tv_backward_f64"):
-            getattr(L, f).restype = ctypes.c_int
-            getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, sz, vp]
-        L.admm_tv_psf_transpose.restype = ctypes.c_int
-        L.admm_tv_psf_transpose.argtypes = [dp, vp, vp, vp, vp, sz, vp]
-        L.admm_tv_profile_enable.restype = ctypes.c_int
-        L.admm_tv_profile_enable.argtypes = [ctypes.c_int]
-        L.admm_tv_profile_reset.restype = ctypes.c_int
-        L.admm_tv_profile_reset.argtypes = []
-        L.admm_tv_profile_read.restype = ctypes.c_int
-        L.admm_tv_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
-        L.admm_tv_last_error.restype = ctypes.c_char_p
-        L.admm_tv_last_error.argtypes = []
-        i64 = ctypes.c_int64
-        L.admm_chanstat_max_channels.restype = ctypes.c_int
-        L.admm_chanstat_max_channels.argtypes = [ctypes.c_int]
-        L.admm_chanstat_pool.restype = ctypes.c_int
-        L.admm_chanstat_pool.argtypes = [ctypes.c_int, vp, i64, i64, i64, vp, vp, vp]
-        L.admm_chanstat_pool_depth.restype = ctypes.c_int
-        L.admm_chanstat_pool_depth.argtypes = [ctypes.c_int, vp, i64, i64, i64, vp, vp, ctypes.c_int, vp]
-        L.admm_chanstat_pool_backward.restype = ctypes.c_int
-        L.admm_chanstat_pool_backward.argtypes = [ctypes.c_int, vp, vp, vp, vp, i64, i64, i64, vp, vp]
-        L.admm_planestat_workspace_size.restype = ctypes.c_int
-        L.admm_planestat_workspace_size.argtypes = [i64, i64, ctypes.POINTER(sz)]
-        L.admm_planestat_median_mode.restype = ctypes.c_int
-        L.admm_planestat_median_mode.argtypes = [ctypes.c_int, vp, i64, i64, vp, vp, vp, sz, ctypes.c_int, vp]
-        L.admm_planestat_select.restype = ctypes.c_int
-        L.admm_planestat_select.argtypes = [ctypes.c_int, vp, i64, i64, vp, vp, vp, vp, sz, ctypes.c_int, vp]
-        if L.admm_tv_abi_version() != ABI_VERSION:
-            raise ImportError("admmtor: native library ABI version mismatch")
-        want, have = source_hash(), L.admm_tv_build_hash().decode()
-        if want is not None and want != have:
-            raise ImportError(f"admmtor: {_LIB_PATH} was built from other sources (build hash {have}, tree "
-                              f"{want}); rebuild it: `python __graft_entry__.py build`")
-        _lib = L
-        return L
+        _lib = _open(_LIB_PATH)
+        return _lib
+
+
+_ab_lib = None
+
+
+@contextlib.contextmanager
+def ab_library():
+    """Tests and tuning only: inside the block every native call of this process goes to the A/B
+    build (AB_LIB_PATH), whose ADMM_* knobs follow the environment, e.g. a solve on the generic kernels
+    at a smooth size (ADMM_MIXED=0) to compare two kernel paths.  Not thread-safe (swaps the module's
+    library handle)."""
+    global _lib, _ab_lib
+    prev = load()
+    with _lock:
+        if _ab_lib is None:
+            _ab_lib = _open(AB_LIB_PATH)
+        _lib = _ab_lib
+    try:
+        yield _ab_lib
+    finally:
+        _lib = prev
+
+
+def _open(path: str) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"admmtor: the HIP library {path} is missing. Build it with "
+            "`python __graft_entry__.py build` (or `make -C torch-admm-deconv_amd/csrc`). "
+            "There is no CPU fallback.")
+    L = ctypes.CDLL(path)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    dp = ctypes.POINTER(AdmmTvDesc)
+    L.admm_tv_abi_version.restype = ctypes.c_int
+    L.admm_tv_abi_version.argtypes = []
+    L.admm_tv_build_hash.restype = ctypes.c_char_p
+    L.admm_tv_build_hash.argtypes = []
+    L.admm_tv_supported.restype = ctypes.c_int
+    L.admm_tv_supported.argtypes = [ctypes.c_int64, ctypes.c_int64]
+    L.admm_tv_supported_f64.restype = ctypes.c_int
+    L.admm_tv_supported_f64.argtypes = [ctypes.c_int64, ctypes.c_int64]
+    L.admm_tv_workspace_size.restype = ctypes.c_int
+    L.admm_tv_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
+    for f in ("admm_tv_forward", "admm_tv_forward_f64"):
+        getattr(L, f).restype = ctypes.c_int
+        getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.admm_tv_history_size.restype = ctypes.c_int
+    L.admm_tv_history_size.argtypes = [dp, ctypes.POINTER(sz)]
+    for f in ("admm_tv_forward_train", "admm_tv_forward_train_f64"):
+        getattr(L, f).restype = ctypes.c_int
+        getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp]
+    L.admm_tv_backward_workspace_size.restype = ctypes.c_int
+    L.admm_tv_backward_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
+    for f in ("admm_tv_backward", "admm_tv_backward_f64"):
+        getattr(L, f).restype = ctypes.c_int
+        getattr(L, f).argtypes = [dp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, sz, vp]
+    L.admm_tv_psf_transpose.restype = ctypes.c_int
+    L.admm_tv_psf_transpose.argtypes = [dp, vp, vp, vp, vp, sz, vp]
+    L.admm_tv_profile_enable.restype = ctypes.c_int
+    L.admm_tv_profile_enable.argtypes = [ctypes.c_int]
+    L.admm_tv_profile_reset.restype = ctypes.c_int
+    L.admm_tv_profile_reset.argtypes = []
+    L.admm_tv_profile_read.restype = ctypes.c_int
+    L.admm_tv_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+    L.admm_tv_last_error.restype = ctypes.c_char_p
+    L.admm_tv_last_error.argtypes = []
+    i64 = ctypes.c_int64
+    L.admm_chanstat_max_channels.restype = ctypes.c_int
+    L.admm_chanstat_max_channels.argtypes = [ctypes.c_int]
+    L.admm_chanstat_pool.restype = ctypes.c_int
+    L.admm_chanstat_pool.argtypes = [ctypes.c_int, vp, i64, i64, i64, vp, vp, vp]
+    L.admm_chanstat_pool_depth.restype = ctypes.c_int
+    L.admm_chanstat_pool_depth.argtypes = [ctypes.c_int, vp, i64, i64, i64, vp, vp, ctypes.c_int, vp]
+    L.admm_chanstat_pool_backward.restype = ctypes.c_int
+    L.admm_chanstat_pool_backward.argtypes = [ctypes.c_int, vp, vp, vp, vp, i64, i64, i64, vp, vp]
+    L.admm_planestat_workspace_size.restype = ctypes.c_int
+    L.admm_planestat_workspace_size.argtypes = [i64, i64, ctypes.POINTER(sz)]
+    L.admm_planestat_median_mode.restype = ctypes.c_int
+    L.admm_planestat_median_mode.argtypes = [ctypes.c_int, vp, i64, i64, vp, vp, vp, sz, ctypes.c_int, vp]
+    L.admm_planestat_select.restype = ctypes.c_int
+    L.admm_planestat_select.argtypes = [ctypes.c_int, vp, i64, i64, vp, vp, vp, vp, sz, ctypes.c_int, vp]
+    if L.admm_tv_abi_version() != ABI_VERSION:
+        raise ImportError("admmtor: native library ABI version mismatch")
+    want, have = source_hash(), L.admm_tv_build_hash().decode()
+    if want is not None and want != have:
+        raise ImportError(f"admmtor: {path} was built from other sources (build hash {have}, tree "
+                          f"{want}); rebuild it: `python __graft_entry__.py build`")
+    return L
 
 
 def check(code: int) -> None:
