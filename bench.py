@@ -537,6 +537,7 @@ def main():
     lam = torch.tensor([0.01], device=dev)
     rho = torch.tensor([0.02], device=dev)
     torch.cuda.synchronize()
+    progress("inputs generated")
 
     # N > 1: the north star's final gather of the whole output over xGMI runs on a side stream and its
     # own process group (its own RCCL communicator / stream), so step k's all_gather overlaps step

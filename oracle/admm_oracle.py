@@ -52,6 +52,7 @@ __all__ = [
     "wiener_factor",
     "solve_spatial",
     "solve_fourier",
+    "solve_fourier_jvp",
     "rel_l2",
 ]
 
@@ -257,6 +258,90 @@ def solve_fourier(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool = 
     if return_state:
         return x, dict(b=b, fc=fc, ux=ux, uy=uy)
     return x
+
+
+def solve_fourier_jvp(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool, maxit: int,
+                      tx: torch.Tensor, tl: torch.Tensor, tr: torch.Tensor):
+    """(y, y_dot): solve_fourier and its directional derivatives along K tangents at once, written out
+    (forward mode, O(state) memory: no graph is kept, so the full config-5 shape fits where the fp64
+    unrolled graph would need ~100 GB).  tx (K, B, C, H, W) are tangents of xin, tl / tr (K,) of lmbd /
+    rho; y_dot is (K, B, C, H, W).  The PSF is held constant.  Torch's derivative conventions for the
+    same expressions (clamp_min passes the derivative at equality, sign and abs have none at 0), so it
+    equals torch.func.jvp of solve_fourier (tests/test_oracle_golden.py checks that at small size).
+
+    Per iteration (deconv.py:103-115, Fourier form):
+      r = b + rho v,  v = Dx^T w_x + Dy^T w_y       r' = b' + rho' v + rho v'
+      x = F^-1 fc F r,  fc = 1/(s2 + rho lap)        x' = F^-1 (fc F r' + fc' F r),  fc' = -fc^2 rho' lap
+      a = D x + u,  z = S(a; tau),  tau = lmbd/rho   a' = D x' + u',  z' = S'(a; tau) (a', tau')
+      u = a - z,  w = z - u"""
+    B, C, H, W = xin.shape
+    dt = xin.dtype
+    K = tx.shape[0]
+    lm = float(lmbd)
+    rh = float(rho)
+    tau = lm / rh
+    tl = tl.to(dt).reshape(K, 1, 1, 1, 1)
+    tr = tr.to(dt).reshape(K, 1, 1, 1, 1)
+    dtau = tl / rh - lm * tr / (rh * rh)
+    if kern.numel() == 0:
+        b, db = xin, tx.to(dt)
+    else:
+        spec = _psf_centered_spectrum(kern.to(dt), H, W)
+        b = torch.fft.irfftn(torch.fft.rfftn(xin, dim=(2, 3)) * spec, s=(H, W), dim=(2, 3))
+        db = torch.fft.irfftn(torch.fft.rfftn(tx.to(dt), dim=(-2, -1)) * spec, s=(H, W), dim=(-2, -1))
+    fc = wiener_factor(H, W, kern, rh, dtype=torch.float64).to(dt)
+    ky = torch.arange(H, dtype=torch.float64).reshape(H, 1)
+    kx = torch.arange(W // 2 + 1, dtype=torch.float64).reshape(1, -1)
+    lap = ((2.0 - 2.0 * torch.cos(2 * math.pi * kx / W)) + (2.0 - 2.0 * torch.cos(2 * math.pi * ky / H))).to(dt)
+    dfc = -(fc * fc * lap) * tr  # (K, 1, 1, H, W/2+1)
+
+    def dxt(a):
+        return a - torch.roll(a, -1, dims=-1)
+
+    def dyt(a):
+        return a - torch.roll(a, -1, dims=-2)
+
+    def dx_(a):
+        return a - torch.roll(a, 1, dims=-1)
+
+    def dy_(a):
+        return a - torch.roll(a, 1, dims=-2)
+
+    def shrink(a, da):
+        if iso:
+            n = torch.sqrt(torch.sum(a * a, dim=(0, 1)) + 1e-15)
+            dn = torch.sum(a * da, dim=(1, 2)) / n           # (K, H, W)
+            ne = n + 1e-15
+            q = 1.0 - tau / ne
+            f = torch.clamp_min(q, 0.0)
+            df = torch.where(q >= 0, -dtau.reshape(K, 1, 1) / ne + tau * dn / (ne * ne), torch.zeros_like(dn))
+            return f * a, f * da + df.unsqueeze(1).unsqueeze(1) * a
+        sg = torch.sign(a)
+        m = torch.abs(a) - tau
+        z = sg * torch.clamp_min(m, 0.0)
+        dz = torch.where(m >= 0, sg * sg * da - sg * dtau, torch.zeros_like(da))
+        return z, dz
+
+    # primal and tangents stacked along a leading axis (index 0 = primal): one FFT call per direction
+    bs = torch.cat([b.unsqueeze(0), db])
+    ux = uy = wx = wy = torch.zeros((K + 1,) + tuple(xin.shape), dtype=dt)
+    xs = ux
+    for _ in range(int(maxit)):
+        v = dxt(wx) + dyt(wy)                            # v_0 and its tangents
+        r = bs + rh * v
+        r[1:] += tr * v[0]
+        Rs = torch.fft.rfftn(r, dim=(-2, -1))
+        Xs = fc * Rs
+        Xs[1:] += dfc * Rs[0]
+        xs = torch.fft.irfftn(Xs, s=(H, W), dim=(-2, -1))
+        ax, ay = dx_(xs) + ux, dy_(xs) + uy
+        zx0, dzx = shrink(ax[0], ax[1:])
+        zy0, dzy = shrink(ay[0], ay[1:])
+        zx = torch.cat([zx0.unsqueeze(0), dzx])
+        zy = torch.cat([zy0.unsqueeze(0), dzy])
+        ux, uy = ax - zx, ay - zy
+        wx, wy = zx - ux, zy - uy
+    return xs[0], xs[1:]
 
 
 def kink_margins(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, maxit: int) -> torch.Tensor:

@@ -96,6 +96,47 @@ def test_grads_reduced_c5_large_tau(cuda_dev):
     assert e[0] <= 1e-5 and e[1] <= 1e-4 and e[2] <= 1e-4 and e[3] <= 1e-4
 
 
+def test_grads_c5_full_shape_forward_mode(cuda_dev):
+    """config 5's gradients at full shape and length (scripts/train.py:19-24: batch-16 512x512x3, iso, no
+    PSF, 100 iterations, learnable lambda / rho as ADMMDeconv(seed 0) draws them): the HIP backward's
+    J^T v against the fp64 oracle's forward-mode derivatives J t (oracle.solve_fourier_jvp: O(state) memory,
+    no unrolled graph), through <J^T v, t> = <v, J t> -- a random direction t in x and the unit directions in
+    lambda and rho, each within 1e-4 relative.  The forward is checked too (<= 1e-5)."""
+    import os
+    from admmtor.eops.deconv import fft_admm_tv
+    from admmtor.synth import blurred_batch
+    from oracle.admm_oracle import solve_fourier_jvp
+    lam0, rho0, it = 0.4963, 0.7682, 100
+    x = blurred_batch(16, 3, 512, 512, torch.empty(0), seed=21)
+    g = torch.Generator().manual_seed(22)
+    v = torch.randn(x.shape, generator=g)
+    t = torch.randn(x.shape, generator=g)
+    xg = x.to(cuda_dev).requires_grad_(True)
+    lam = torch.tensor([lam0], device=cuda_dev, requires_grad=True)
+    rho = torch.tensor([rho0], device=cuda_dev, requires_grad=True)
+    out = fft_admm_tv(xg, lam, rho, torch.empty(0, device=cuda_dev), True, it)
+    gx, gl, gr = torch.autograd.grad(out, (xg, lam, rho), v.to(cuda_dev))
+    torch.cuda.synchronize()
+    hip = (torch.dot(gx.double().cpu().flatten(), t.double().flatten()).item(), gl.double().item(), gr.double().item())
+    out = out.detach().cpu()
+    del xg, gx
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    x64 = x.double()
+    tx = torch.zeros((3,) + tuple(x.shape), dtype=torch.float64)
+    tx[0] = t.double()
+    # the fp32 parameters' exact values (the HIP solve reads lambda / rho as fp32)
+    lam32, rho32 = float(torch.tensor(lam0, dtype=torch.float32)), float(torch.tensor(rho0, dtype=torch.float32))
+    y, ydot = solve_fourier_jvp(x64, lam32, rho32, torch.empty(0, dtype=torch.float64),
+                                True, it, tx, torch.tensor([0.0, 1.0, 0.0]), torch.tensor([0.0, 0.0, 1.0]))
+    ref = [torch.dot(v.double().flatten(), ydot[i].flatten()).item() for i in range(3)]
+    e_fwd = rel(out, y)
+    errs = [abs(h - r) / abs(r) for h, r in zip(hip, ref)]
+    print(f"C5 full shape, 100 it: forward {e_fwd:.3e}; <x^, t> {hip[0]:.6e} vs {ref[0]:.6e}, lambda^ {hip[1]:.6e} vs "
+          f"{ref[1]:.6e}, rho^ {hip[2]:.6e} vs {ref[2]:.6e}; rel {errs[0]:.2e} {errs[1]:.2e} {errs[2]:.2e}")
+    assert e_fwd <= 1e-5
+    assert max(errs) <= 1e-4
+
+
 def test_maxit_zero_grads_are_zero(cuda_dev):
     from admmtor.eops.deconv import fft_admm_tv
     x = torch.rand(1, 2, 32, 32, device=cuda_dev, requires_grad=True)

@@ -108,3 +108,47 @@ def test_iso_couples_the_batch():
     full = solve_fourier(x, 0.03, 0.05, torch.empty(0, dtype=torch.float64), True, 40)
     one = solve_fourier(x[:1], 0.03, 0.05, torch.empty(0, dtype=torch.float64), True, 40)
     assert rel_l2(one, full[:1]) > 1e-4
+
+
+def test_forward_mode_oracle_pinned_by_reference_gradients():
+    """oracle.solve_fourier_jvp (the forward-mode checker of the full-shape config-5 gradient test) is
+    pinned to the reference's own fp64 autograd (g4: train config, iso, 100 iterations): with the
+    reference's vector-Jacobian products gx, glam, grho for the cotangent c, <c, J t> = <gx, t_x> +
+    glam t_lam + grho t_rho for every direction t."""
+    from oracle.admm_oracle import solve_fourier_jvp
+    g = load_golden("g4_train_grad")
+    x = T(g["x"])
+    gen = torch.Generator().manual_seed(5)
+    tx = torch.zeros((3,) + tuple(x.shape), dtype=torch.float64)
+    tx[0] = torch.randn(x.shape, generator=gen, dtype=torch.float64)
+    y, yd = solve_fourier_jvp(x, float(g["lam"][0]), float(g["rho"][0]), torch.empty(0, dtype=torch.float64), True,
+                              int(g["maxit"]), tx, torch.tensor([0.0, 1.0, 0.0]), torch.tensor([0.0, 0.0, 1.0]))
+    assert rel_l2(y, T(g["out"])) <= 1e-10
+    c = T(g["cot"]).flatten()
+    got = [torch.dot(c, yd[i].flatten()).item() for i in range(3)]
+    want = [torch.dot(T(g["gx"]).flatten(), tx[0].flatten()).item(), float(g["glam"][0]), float(g["grho"][0])]
+    for a, b in zip(got, want):
+        assert abs(a - b) <= 1e-9 * max(1.0, abs(b)), (got, want)
+
+
+@pytest.mark.parametrize("iso", [False, True])
+def test_forward_mode_oracle_is_torch_jvp(iso):
+    """solve_fourier_jvp's written-out tangents equal torch.func.jvp through solve_fourier (PSF and
+    no PSF), all three tangent kinds at once."""
+    from oracle.admm_oracle import solve_fourier_jvp
+    gen = torch.Generator().manual_seed(1)
+    for kern in (torch.empty(0, dtype=torch.float64), torch.rand(1, 1, 5, 5, generator=gen, dtype=torch.float64)):
+        x = torch.rand(2, 3, 24, 20, generator=gen, dtype=torch.float64)
+        lam, rho = torch.tensor(0.05, dtype=torch.float64), torch.tensor(0.3, dtype=torch.float64)
+        tx = torch.stack([torch.randn(x.shape, generator=gen, dtype=torch.float64), torch.zeros_like(x),
+                          torch.randn(x.shape, generator=gen, dtype=torch.float64)])
+        tl = torch.tensor([0.0, 1.0, 0.4], dtype=torch.float64)
+        tr = torch.tensor([0.0, 0.0, -0.7], dtype=torch.float64)
+        y, yd = solve_fourier_jvp(x, lam, rho, kern, iso, 12, tx, tl, tr)
+
+        def f(tt):
+            return torch.func.jvp(lambda a, lm, r: solve_fourier(a, lm, r, kern, iso, 12), (x, lam, rho), tt)[1]
+        ref = torch.vmap(f)((tx, tl, tr))
+        assert rel_l2(y, solve_fourier(x, lam, rho, kern, iso, 12)) <= 1e-14
+        for i in range(3):
+            assert rel_l2(yd[i], ref[i]) <= 1e-12
