@@ -81,14 +81,32 @@ __device__ __forceinline__ double soft_dtau(double a, double zb, double tau) {
     return (fabs(a) > tau) ? (a > 0.0 ? -zb : zb) : 0.0;
 }
 
+// Row transform configuration of the reverse row pass.  Its lanes carry five row states (r^ of two
+// rows, a^_x of the previous row, a^_y of two rows) besides the transform, so at the forward's E values
+// per lane the 256-point rows (W = 512: config 5) needed 229 VGPRs iso -- two waves per SIMD, and the
+// latency-bound pass ran at 0.33 of the HBM peak (SQ: an instruction in flight 26 % of the cycles).
+// 256-point rows run here with 4 values per lane over a full wave (4 * 4 * 4 * 4: one more LDS exchange
+// per transform), which halves the state registers.
+template <int N> struct BwdCfg : RowCfg<N> {};
+template <> struct BwdCfg<256> {
+    static constexpr int E = 4;
+    using S = Sched<4, 4, 4, 4>;
+};
+template <int N> struct BwdGeom {
+    static constexpr int E = BwdCfg<N>::E, L = N / E, W = 2 * N;
+    static constexpr int NT = 256, SG = NT / L;
+    static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * RowBuf::slots(N)); }
+};
+
 // occupancy target of the reverse row pass (waves per SIMD), as PASSA_MINW for the forward:
 // 3 for aniso (measured -2.4 % at C3 size; a few registers spill), 2 for iso, whose extra
-// norm / Q operands would spill ~240 B at 3 (measured +4 %)
-#define BWDA_MINW(n, iso) ((n) >= 1024 ? 1 : (iso) ? 2 : 3)
+// norm / Q operands would spill ~240 B at 3 (measured +4 %); the 4-value 256-point rows fit 3 iso
+#define BWDA_MINW(n, iso) ((n) >= 1024 ? 1 : (n) == 256 ? 3 : (iso) ? 2 : 3)
 
 template <int N, bool ISO, bool LASTK, bool FIRSTK>
 __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a) {
-    using G = RowKernelGeom<N>;
+    using G = BwdGeom<N>;
+    using Xf = RowXf<N, BwdCfg<N>>;
     constexpr int E = G::E, L = G::L, W = G::W;
     // streaming history / adjoint images and the spectra non-temporal, as the forward's pass A;
     // the per-module norm and Q maps (re-read by every plane) stay cacheable
@@ -137,14 +155,14 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
         const int g = (i0 - 1 + H) & (H - 1);
 #pragma unroll
         for (int j = 0; j < E; ++j) rprev[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + L * j]);
-        RowXf<N>::c2r(rprev, buf, tw, t);
+        Xf::c2r(rprev, buf, tw, t);
     }
     for (int rr = 0; rr <= R; ++rr) {
         const int g = (i0 + rr) & (H - 1);
         const size_t ro = (size_t)g * N;
 #pragma unroll
         for (int j = 0; j < E; ++j) rcur[j] = ld_pol<kSpecNT>(&sp[ro + t + L * j]);
-        RowXf<N>::c2r(rcur, buf, tw, t);
+        Xf::c2r(rcur, buf, tw, t);
 
         // ---- y direction at row g
         cf abyc[E];
@@ -213,7 +231,7 @@ __global__ void __launch_bounds__(256, BWDA_MINW(N, ISO)) k_bwd_pass_a(BwdArgs a
                     r[j] = mkc((abxp[j].x - abxp[j].y) + (abyp[j].x - abyc[j].x),
                                (abxp[j].y - ar) + (abyp[j].y - abyc[j].y));
                 }
-                RowXf<N>::r2c(r, buf, tw, t);
+                Xf::r2c(r, buf, tw, t);
 #pragma unroll
                 for (int j = 0; j < E; ++j) st_pol<kNT>(&so[rm + t + L * j], r[j]);
             }

@@ -318,10 +318,11 @@ template <int N> struct RowOps {
         return launch_check("k_iso_norm");
     }
     template <bool ISO, bool LASTK, bool FIRSTK> static void bpa(const BwdArgs& a, unsigned nb, hipStream_t s) {
-        hipLaunchKernelGGL((k_bwd_pass_a<N, ISO, LASTK, FIRSTK>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        using BG = BwdGeom<N>;
+        hipLaunchKernelGGL((k_bwd_pass_a<N, ISO, LASTK, FIRSTK>), dim3(nb), dim3(BG::NT), BG::lds_bytes(), s, a);
     }
     static int bwd_pass_a(const BwdArgs& a, bool iso, bool lastk, bool firstk, hipStream_t s) {
-        const unsigned nb = blocks(a.nstrips);
+        const unsigned nb = (unsigned)((a.nstrips + BwdGeom<N>::SG - 1) / BwdGeom<N>::SG);  // its own strips per block
         const int sel = (iso ? 4 : 0) | (lastk ? 2 : 0) | (firstk ? 1 : 0);
         switch (sel) {
             case 0: bpa<false, false, false>(a, nb, s); break;

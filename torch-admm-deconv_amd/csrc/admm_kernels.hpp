@@ -22,8 +22,10 @@ namespace admm {
 // ---------------------------------------------------------------------------
 // packed real-row transforms for one sub-group of L lanes (natural layout)
 // ---------------------------------------------------------------------------
-template <int N> struct RowXf {
-    static constexpr int E = RowCfg<N>::E;
+// Cfg: values per lane E and the radix schedule S (RowCfg<N> by default; the training backward's row
+// pass runs the 256-point rows with fewer values per lane, admm_backward.hpp BwdCfg)
+template <int N, class Cfg = RowCfg<N>> struct RowXf {
+    static constexpr int E = Cfg::E;
     static constexpr int L = N / E;
     static constexpr int W = 2 * N;
     static_assert(L <= 64, "row transforms keep one row inside one wave");
@@ -58,12 +60,12 @@ template <int N> struct RowXf {
             }
             v[j] = z;
         }
-        fft<N, L, +1, 0, 2>(v, buf, tw, t);
+        fft_e<N, L, E, +1, 0, 2>(v, buf, tw, t, typename Cfg::S{});
     }
 
     // pixel pairs of a real row r -> packed spectrum 2*rfft(r)
     __device__ __forceinline__ static void r2c(cf (&v)[E], const RowBuf& buf, const cf* __restrict__ tw, int t) {
-        fft<N, L, -1, 0, 2>(v, buf, tw, t);
+        fft_e<N, L, E, -1, 0, 2>(v, buf, tw, t, typename Cfg::S{});
         cf p[E];
         partner(v, p, t);
 #pragma unroll

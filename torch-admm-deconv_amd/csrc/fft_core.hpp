@@ -330,6 +330,12 @@ __device__ __forceinline__ void fft_dispatch(cf (&v)[RowCfg<N>::E], const Buf& b
     run_sched<N, L, RowCfg<N>::E, 1, DIR, true, SYNC, TWMUL, Buf, Rs...>(v, buf, tw, t);
 }
 
+// the same with E values per lane and an explicit schedule (each radix divides E)
+template <int N, int L, int E, int DIR, int SYNC, int TWMUL, class Buf, int... Rs>
+__device__ __forceinline__ void fft_e(cf (&v)[E], const Buf& buf, const cf* __restrict__ tw, int t, Sched<Rs...>) {
+    run_sched<N, L, E, 1, DIR, true, SYNC, TWMUL, Buf, Rs...>(v, buf, tw, t);
+}
+
 // Full N-point complex FFT (DIR -1 forward / +1 inverse, unnormalised) in natural layout.
 template <int N, int L, int DIR, int SYNC, int TWMUL, class Buf>
 __device__ __forceinline__ void fft(cf (&v)[RowCfg<N>::E], const Buf& buf, const cf* __restrict__ tw, int t) {
