@@ -1,11 +1,13 @@
 #!/bin/bash
-# Interleaved A/B of environment knobs on one bench config (the knobs are read only by an A/B build of the
-# library, csrc/knobs.hpp: bash tools/build_variant.sh ab, then ADMMTOR_LIB_OVERRIDE=tools/_variants/ab.so): bench.py --config <cfg> for each setting, two
-# rounds, each run under its own time limit; the bench's JSON line (value, roofline) per run.
+# Interleaved A/B of environment knobs on one bench config: bench.py --config <cfg> for each setting, two
+# rounds, each run under its own time limit; the bench's JSON line (value, roofline) per run.  The knobs are
+# read only by the A/B build of the library (csrc/knobs.hpp), which this script loads
+# (admmtor/_lib/libadmm_tv_ab.so, built by the Makefile) unless ADMMTOR_LIB_OVERRIDE is set.
 # usage: bash tools/gpu_ab_env.sh <config> "A=1 B=2" "A=0 B=2" ...   -> gpurun_out/ab_env_<config>.txt
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
+export ADMMTOR_LIB_OVERRIDE=${ADMMTOR_LIB_OVERRIDE:-$GRAFT_REPO_ROOT/torch-admm-deconv_amd/admmtor/_lib/libadmm_tv_ab.so}
 CFG=$1; shift
 OUT=gpurun_out/ab_env_$CFG.txt
 mkdir -p gpurun_out

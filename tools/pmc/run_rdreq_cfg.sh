@@ -1,12 +1,13 @@
 #!/bin/bash
 # HBM bytes per kernel (memory-side request-size counters, as run_rdreq.sh) for one bench config
 # (bsd, hd, c2, ...), one stream (ADMM_GEN_STREAMS=1), 1 step + 1 warm-up, plus the calibration copies.
-# usage: bash tools/pmc/run_rdreq_cfg.sh <config>   -> gpurun_out/rdreq_<config>/
+# usage: bash tools/pmc/run_rdreq_cfg.sh <config> [tag]   -> gpurun_out/rdreq_<config>[_<tag>]/
+# (A/B knobs: run it with ADMMTOR_LIB_OVERRIDE=<the A/B library> and the knob in the environment)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 CFG=${1:-bsd}
-OUT="$GRAFT_REPO_ROOT/gpurun_out/rdreq_$CFG"
+OUT="$GRAFT_REPO_ROOT/gpurun_out/rdreq_$CFG${2:+_$2}"
 mkdir -p "$OUT"
 python3 -c "import sys; sys.path.insert(0, 'torch-admm-deconv_amd'); from admmtor import _native; print(_native.load().admm_tv_build_hash().decode())" > "$OUT/build_hash.txt" || exit 1
 RD="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
