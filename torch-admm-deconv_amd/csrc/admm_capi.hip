@@ -200,7 +200,7 @@ Layout make_layout(const admm_tv_desc& d) {
     L.twHd = take(H * sizeof(double2));
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
     L.gscr = L.gen ? take(glb_scratch((int)H, (int)W, (long long)P, f64)) : 0;
-    L.fcM = L.mixed ? take((N + 1) * H * sizeof(float)) : 0;  // [H][N + 1], k_fc_mixed
+    L.fcM = L.mixed ? take((2 * N + 1) * H * sizeof(float)) : 0;  // [H][N + 1] + packed copy, k_fc_mixed
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
         // plane groups for the iso norm pass: enough (group,row) items to fill the chip

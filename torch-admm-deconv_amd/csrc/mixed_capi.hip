@@ -169,12 +169,24 @@ hipError_t iso_norm(int N, const IsoArgs& a, bool first, hipStream_t s) {
     });
 }
 
+int pass_b_cols(int H, int N) {
+    int cols = 0;
+    (void)with_col(H, [&](auto h) {
+        constexpr int C0 = MCol<decltype(h)::value>::C;
+        cols = N % C0 == 0 ? C0 : (C0 > 4 && N % 4 == 0) ? 4 : (C0 > 2 && N % 2 == 0) ? 2 : 0;
+        return hipSuccess;
+    });
+    return cols;
+}
+
 hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s) {
     return with_col(H, [&](auto h) {
         constexpr int HH = decltype(h)::value;
-        // plane groups of two at H >= 1024 (k_pass_b's measured tile order), plane-major below; A/B knob
-        // ADMM_PASSB_M_ORDER (read once per process: it changes no sizes)
+        // plane groups of two at H >= 1024 (k_pass_b's measured tile order), plane-major below; A/B knobs
+        // ADMM_PASSB_M_ORDER, ADMM_PASSB_M_FPACK (the column-block-packed factors; read once per process:
+        // they change no sizes)
         static const int forced = env_int("ADMM_PASSB_M_ORDER", 0);
+        static const int fpack = env_int("ADMM_PASSB_M_FPACK", 1);
         const int order = forced > 0 ? forced : (HH >= 1024 ? 2 : 1);
         auto go = [&](auto cc) {
             constexpr int CC = decltype(cc)::value;
@@ -182,7 +194,7 @@ hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long 
             const int colblocks = N / CC;
             if (hipError_t e = lds(k_pass_b_m<HH, CC>, G::lds_bytes())) return e;
             hipLaunchKernelGGL((k_pass_b_m<HH, CC>), dim3((unsigned)(P * colblocks)), dim3(G::NT), G::lds_bytes(), s,
-                               spec, fcM, twH, N, colblocks, order);
+                               spec, fcM, twH, N, colblocks, order, fpack);
             return hipGetLastError();
         };
         // the plan's columns per block, or fewer when N is no multiple of them (e.g. W = 1080 beside the
@@ -200,9 +212,11 @@ hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long 
 }
 
 hipError_t fc_mixed(const float* fcT, float* fcM, int H, int N, hipStream_t s) {
-    const long long n = (long long)H * (N + 1);
+    const long long n = (long long)H * (2 * N + 1);
+    const int C = pass_b_cols(H, N);
+    if (C <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_fc_mixed, dim3((unsigned)std::min<long long>(4096, (n + 255) / 256)), dim3(256), 0, s, fcT, fcM,
-                       H, N);
+                       H, N, C);
     return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@ using admm::cf;
 bool row_ok(int N);
 bool col_ok(int H);
 int col_cols(int H);  // the fewest columns per column-pass block (N must be a multiple)
+int pass_b_cols(int H, int N);  // the columns per block pass_b launches (0: N fits no plan)
 int row_lanes(int N);  // lanes of a row group (up to 256: several waves)
 int pass_a_blocks_per_cu(int N);  // resident 256-thread blocks of the row pass per CU (occupancy query)
 
@@ -22,6 +23,7 @@ hipError_t c2r(int N, const cf* spec, float* img, const cf* twW, long long rows,
 hipError_t pass_a(int N, const admm::PassAArgs& a, bool iso, bool first, hipStream_t s);
 hipError_t iso_norm(int N, const admm::IsoArgs& a, bool first, hipStream_t s);
 hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s);
+// fcM: [H][N + 1] then the column-block-packed copy [N / C][H][C] (C = pass_b_cols): H (2N + 1) floats
 hipError_t fc_mixed(const float* fcT, float* fcM, int H, int N, hipStream_t s);
 
 }  // namespace admm_mixed

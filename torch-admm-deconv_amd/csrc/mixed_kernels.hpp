@@ -458,12 +458,21 @@ __global__ void __launch_bounds__(256) k_row_c2r_m(const cf* __restrict__ spec, 
 
 // Wiener factor for the mixed column pass: fcM[ky][kx] = fcT[kx][ky] / 2 (kx in [0, N], row-major so a
 // block's C adjacent columns read adjacent factors; the / 2 turns the generic path's 1/(HW) scale into
-// the packed row transforms' 1/(2HW), exactly)
-static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restrict__ fcM, int H, int N) {
-    const long long n = (long long)H * (N + 1);
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-        const int ky = (int)(i / (N + 1)), kx = (int)(i % (N + 1));
-        fcM[i] = 0.5f * fcT[(size_t)kx * H + ky];
+// the packed row transforms' 1/(2HW), exactly), followed by the column-block-packed copy
+// fcP[cb][ky][c] = fcM[ky][cb C + c] (kx < N): a block's factors are one contiguous C H run, so a wave
+// reads whole lines and no line is shared with the neighbouring column blocks (which may run on other XCDs)
+static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restrict__ fcM, int H, int N, int C) {
+    const long long n = (long long)H * (N + 1), np = (long long)H * N;
+    float* fcP = fcM + n;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n + np; i += (long long)gridDim.x * blockDim.x) {
+        if (i < n) {
+            const int ky = (int)(i / (N + 1)), kx = (int)(i % (N + 1));
+            fcM[i] = 0.5f * fcT[(size_t)kx * H + ky];
+        } else {
+            const long long j = i - n;  // (cb, ky, c)
+            const int c = (int)(j % C), ky = (int)((j / C) % H), cb = (int)(j / ((long long)C * H));
+            fcP[j] = 0.5f * fcT[(size_t)(cb * C + c) * H + ky];
+        }
     }
 }
 
@@ -476,7 +485,8 @@ static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restri
 // target for the smooth column plans (capped registers spill and lose 4-21 %).
 template <int H, int CC>
 __global__ void __launch_bounds__((MColG<H, CC>::NT))
-k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g, int N, int colblocks, int order) {
+k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g, int N, int colblocks, int order,
+           int fpack) {
     using G = MColG<H, CC>;
     constexpr int Lc = G::Lc, Ec = G::Ec, C = G::C, EM = G::EM, NBz = G::NBz, Qz = G::Qz;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -497,13 +507,17 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
     for (int j = 0; j < Ec; ++j) v[j] = bload_cf(rs, voff, j * sstep);
     // frequencies in layout(Rz): v[q + Qz k] <-> ky = t + Lc q + NBz k (valid for t + Lc q < NBz)
     float m[EM];
+    // the factors of this thread's column: from the column-block-packed copy (k_fc_mixed) or the
+    // row-major table
+    const float* fcP = fcM + (size_t)H * (N + 1) + (size_t)cb * H * C + c;
     auto load_m = [&]() {
 #pragma unroll
         for (int q = 0; q < Qz; ++q) {
             const int vt = t + Lc * q;
 #pragma unroll
             for (int k = 0; k < G::Rz; ++k)
-                m[q + Qz * k] = (vt < NBz) ? fcM[(size_t)(vt + NBz * k) * (N + 1) + col] : 0.f;
+                m[q + Qz * k] = (vt < NBz) ? (fpack ? fcP[(size_t)(vt + NBz * k) * C]
+                                                    : fcM[(size_t)(vt + NBz * k) * (N + 1) + col]) : 0.f;
         }
     };
     __syncthreads();  // twiddles in LDS
