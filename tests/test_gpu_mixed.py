@@ -98,23 +98,79 @@ def test_mixed_planes_independent(cuda_dev):
     assert torch.equal(full[1:2, 1:2], one)
 
 
-def test_mixed_autograd_uses_generic_training(cuda_dev):
-    """Training at a smooth size: the forward with history and the backward run on the generic kernels
-    (the inference solve on the fused mixed kernels); the output of the training forward equals the
-    generic inference solve and its gradients match the oracle's autograd."""
+TRAIN_CASES = [
+    # (B, C, H, W), psf (fixed), iso, iterations
+    ((1, 2, 240, 480), None, True, 8),                 # 240-point rows over a 32-lane group
+    ((1, 1, 360, 720), ("gauss:1.5", 5), False, 10),   # 360-point rows, a fixed PSF (x^_in = H_t^T b^)
+    ((2, 1, 360, 800), None, True, 6),                 # 400-point rows, two planes coupled by the iso norm
+    ((1, 1, 240, 1920), ("motion", 5), False, 6),      # HD rows: a wide row group of 2 waves (960 = 8 15 8)
+    ((1, 1, 256, 1280), None, True, 6),                # 720p rows (wide, 640 = 10 8 8) beside power-of-two columns
+]
+
+
+@pytest.mark.parametrize("shape,psf,iso,it", TRAIN_CASES)
+def test_mixed_training_gradients_vs_oracle(cuda_dev, monkeypatch, shape, psf, iso, it):
+    """Training at smooth sizes runs on the mixed kernels (forward with history: k_pass_a_m / k_iso_norm_m
+    with HIST; backward: the inference column pass + k_bwd_pass_a_m / k_bwd_iso_q_m): output, x, lambda
+    and rho gradients against the fp64 oracle's autograd (deconv.py:103-115), and against the same training
+    step on the generic kernels (the A/B build, ADMM_MIXED=0)."""
+    from admmtor import _native
     from admmtor.eops.deconv import fft_admm_tv
-    from admmtor.synth import blurred_batch
+    from admmtor.synth import blurred_batch, make_psf
     from oracle.admm_oracle import solve_fourier
-    x = blurred_batch(1, 2, 240, 480, torch.empty(0), seed=8)
+    assert _native.load().admm_tv_supported(shape[2], shape[3]) == 3
+    k = make_psf(*psf) if psf else None
+    x = blurred_batch(*shape, k if k is not None else torch.empty(0), seed=sum(shape) + 3)
     cot = torch.randn(x.shape, generator=torch.Generator().manual_seed(1))
-    xg = x.to(cuda_dev).requires_grad_(True)
-    lam = torch.tensor([0.03], device=cuda_dev, requires_grad=True)
-    out = fft_admm_tv(xg, lam, 0.05, torch.empty(0, device=cuda_dev), True, 8)
-    gx, gl = torch.autograd.grad(out, (xg, lam), cot.to(cuda_dev))
+
+    def hip():
+        xg = x.to(cuda_dev).requires_grad_(True)
+        lam = torch.tensor([0.03], device=cuda_dev, requires_grad=True)
+        rho = torch.tensor([0.05], device=cuda_dev, requires_grad=True)
+        kk = k.to(cuda_dev) if k is not None else torch.empty(0, device=cuda_dev)
+        out = fft_admm_tv(xg, lam, rho, kk, iso, it)
+        g = torch.autograd.grad(out, (xg, lam, rho), cot.to(cuda_dev))
+        torch.cuda.synchronize()
+        return [out.detach().cpu()] + [v.cpu() for v in g]
+    got = hip()
+    monkeypatch.setenv("ADMM_MIXED", "0")
+    with _native.ab_library():
+        gen = hip()
     xr = x.double().requires_grad_(True)
     lr = torch.tensor([0.03], dtype=torch.float64, requires_grad=True)
-    ref = solve_fourier(xr, lr, 0.05, torch.empty(0, dtype=torch.float64), True, 8)
-    rgx, rgl = torch.autograd.grad(ref, (xr, lr), cot.double())
-    e = (rel(out.detach().cpu(), ref.detach()), rel(gx.cpu(), rgx), rel(gl.cpu(), rgl))
-    print("240x480 training:", e)
-    assert e[0] <= TOL_REF64 and e[1] <= 1e-4 and e[2] <= 1e-4
+    rr = torch.tensor([0.05], dtype=torch.float64, requires_grad=True)
+    kr = k.double() if k is not None else torch.empty(0, dtype=torch.float64)
+    ref = solve_fourier(xr, lr, rr, kr, iso, it)
+    want = [ref.detach()] + list(torch.autograd.grad(ref, (xr, lr, rr), cot.double()))
+    e = [rel(a, b) for a, b in zip(got, want)]
+    eg = [rel(a, b) for a, b in zip(gen, want)]
+    print(shape, psf, "iso" if iso else "aniso", it, "mixed (out, x, lam, rho):", ["%.2e" % v for v in e],
+          "generic:", ["%.2e" % v for v in eg])
+    assert e[0] <= TOL_REF64 and max(e[1:]) <= 1e-4
+    assert not torch.equal(got[1], gen[1])  # the mixed kernels ran, not the generic ones
+
+
+def test_mixed_size_psf_gradient_uses_generic_history(cuda_dev):
+    """A PSF gradient at a smooth size keeps the generic training path (its column-spectrum history):
+    x, lambda, rho and PSF gradients against the fp64 oracle's autograd."""
+    from admmtor.eops.deconv import fft_admm_tv
+    from admmtor.synth import blurred_batch, make_psf
+    from oracle.admm_oracle import solve_spatial  # the reference's op sequence: autograd reaches the PSF
+    k = make_psf("motion", 5)
+    x = blurred_batch(1, 1, 240, 480, k, seed=9)
+    cot = torch.randn(x.shape, generator=torch.Generator().manual_seed(2))
+    xg = x.to(cuda_dev).requires_grad_(True)
+    lam = torch.tensor([0.03], device=cuda_dev, requires_grad=True)
+    rho = torch.tensor([0.05], device=cuda_dev, requires_grad=True)
+    kg = k.to(cuda_dev).requires_grad_(True)
+    out = fft_admm_tv(xg, lam, rho, kg, False, 6)
+    got = [out.detach().cpu()] + [v.cpu() for v in torch.autograd.grad(out, (xg, lam, rho, kg), cot.to(cuda_dev))]
+    xr = x.double().requires_grad_(True)
+    lr = torch.tensor([0.03], dtype=torch.float64, requires_grad=True)
+    rr = torch.tensor([0.05], dtype=torch.float64, requires_grad=True)
+    kr = k.double().requires_grad_(True)
+    ref = solve_spatial(xr, lr, rr, kr, False, 6)
+    want = [ref.detach()] + list(torch.autograd.grad(ref, (xr, lr, rr, kr), cot.double()))
+    e = [rel(a, b) for a, b in zip(got, want)]
+    print("240x480 PSF gradient:", ["%.2e" % v for v in e])
+    assert e[0] <= TOL_REF64 and max(e[1:]) <= 1e-3

@@ -430,7 +430,7 @@ __global__ void k_bwd_scalars(const double* __restrict__ part, int K, long long 
 }
 
 // sum of the modules' b^ images: out[i] = sum_g in[g n + i] (fixed order)
-__global__ void k_sum_modules(const float4* __restrict__ in, float4* __restrict__ out, int G, long long n4) {
+static __global__ void k_sum_modules(const float4* __restrict__ in, float4* __restrict__ out, int G, long long n4) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     float4 s = in[i];
@@ -544,7 +544,7 @@ __global__ void __launch_bounds__(C * (H / RowCfg<H>::E), 1)
 }
 
 // acc[f] += sum_g part[g][f] * (fcT ? fcT[f]^2 real part : complex), in fp64 (f over (N+1)*H)
-__global__ void k_xspec_reduce(const cf* __restrict__ part, int ngroups, long long nf, const float* __restrict__ fcT,
+static __global__ void k_xspec_reduce(const cf* __restrict__ part, int ngroups, long long nf, const float* __restrict__ fcT,
                                double2* __restrict__ acc) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nf) return;

@@ -145,8 +145,10 @@ struct Layout {
     // generic path: the matrix-core plans, decided once per call (their environment knobs are read
     // here only, so the regions sized below and the kernels launched later always agree)
     MMPlan mm, mmr;
-    // mixed-radix fused inference (mixed_hw; run_forward_mixed): the Wiener factor for its column pass
-    bool mixed;
+    // mixed-radix fused iteration (mixed_hw; run_forward_mixed): the Wiener factor for its column pass.
+    // mixed_train: training forward / backward on it too (not with a PSF gradient, whose column-spectrum
+    // history is the generic path's)
+    bool mixed, mixed_train;
     size_t fcM;
     size_t rimg;  // generic path: spec[0] = half spectra [P][H][W/2+1], spec[1] = x image, rimg = r image
     size_t gscr;  // generic path, lines beyond the LDS image: the transform blocks' scratch slots
@@ -179,6 +181,7 @@ Layout make_layout(const admm_tv_desc& d) {
         L.mmr = mm_plan_row((int)W);
     }
     L.mixed = L.gen && !f64 && G == 1 && mixed_hw(d.H, d.W);
+    L.mixed_train = L.mixed && !(k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD));
     L.ldw = (int)(N + 1);
     if (L.gen && !f64 && L.mm.ok && L.mmr.ok && env_int("ADMM_GEN_PITCH", 1)) L.ldw = (int)((N + 1 + 15) / 16 * 16);
     L.spec[0] = take(L.gen ? P * H * (size_t)L.ldw * csz : img);
@@ -1493,10 +1496,12 @@ long long mixed_slots(int N) {
     cache.push_back({{dev, N}, slots});
     return slots;
 }
-int strip_rows_mixed(int H, long long rows, int N) {
+// slots <= 0: this device's (mixed_slots); the training backward's layout passes a fixed count (its
+// workspace size must not depend on the device)
+int strip_rows_mixed(int H, long long rows, int N, long long slots = 0) {
     if (const int e = env_int("ADMM_MIXED_R", 0); e > 0 && H % e == 0) return e;
     const int sg = 256 / std::max(1, admm_mixed::row_lanes(N));  // strips per block
-    const long long slots = mixed_slots(N);
+    if (slots <= 0) slots = mixed_slots(N);
     int best = 1;
     double best_t = 1e300;
     for (int R = 1; R <= 32 && R <= H; ++R) {
@@ -1518,9 +1523,19 @@ int strip_rows_mixed(int H, long long rows, int N) {
 // factor, column IFFT), [iso: the norm pass, its reduce and the cross-rank hook], pass A -- inside
 // the generic layout's regions (spec[0] / spec[1] hold the packed row spectra ping-pong, u[0..3] the
 // u images; the generic b region or xin is b, in pixel order).
+// hist: the training forward (Layout::mixed_train) -- a_k and N_k into the history as run_forward's
+// fused loop writes them (make_hist), and the last iteration's pass A also runs.
 int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin, const float* lam, const float* rho,
-                      float* out, void* ws, hipStream_t s) {
+                      float* out, void* ws, void* hist, hipStream_t s) {
     const long long P = d.B * d.C;
+    const bool train = hist != nullptr;
+    const Hist Hs = make_hist(d);
+    auto ha = [&](int k, int comp) -> float* {  // a_k image (k >= 1), comp 0 = x, 1 = y
+        return reinterpret_cast<float*>(static_cast<char*>(hist) + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
+    };
+    auto hn = [&](int k) -> float* {  // N_k (k >= 1)
+        return reinterpret_cast<float*>(static_cast<char*>(hist) + Hs.n_off + (size_t)(k - 1) * Hs.n_slot);
+    };
     const int H = (int)d.H, W = (int)d.W, N = W / 2;
     cf* twW = at<cf>(ws, Lo.twW);
     cf* twH = at<cf>(ws, Lo.twH);
@@ -1550,20 +1565,31 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
         }
         if (it == d.maxit) {
             ProfScope ps(3, s);
-            return hchk(admm_mixed::c2r(N, spec[cur], out, twW, rows, s), "k_row_c2r_m");
+            if (int e = hchk(admm_mixed::c2r(N, spec[cur], out, twW, rows, s), "k_row_c2r_m")) return e;
+            if (!train) return 0;
         }
         const bool first = it == 1;
-        const float* uxi = u[2 * uin];
-        const float* uyi = u[2 * uin + 1];
-        float* uxo = u[2 * (1 - uin)];
-        float* uyo = u[2 * (1 - uin) + 1];
+        const float *uxi, *uyi, *nprev = nullptr;
+        float *uxo, *uyo;
+        if (train) {  // a_{k-1} in, a_k out (u is rebuilt from a in the kernels)
+            uxi = first ? nullptr : ha(it - 1, 0);
+            uyi = first ? nullptr : ha(it - 1, 1);
+            uxo = ha(it, 0);
+            uyo = ha(it, 1);
+            if (d.iso && !first) nprev = hn(it - 1);
+        } else {
+            uxi = u[2 * uin];
+            uyi = u[2 * uin + 1];
+            uxo = u[2 * (1 - uin)];
+            uyo = u[2 * (1 - uin) + 1];
+        }
         const float* nsq = nullptr;
         if (d.iso) {
             ProfScope ps(2, s);
-            float* nout = at<float>(ws, Lo.nsq);
-            IsoArgs ia{spec[cur], uxi, uyi, nullptr, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
+            float* nout = train ? hn(it) : at<float>(ws, Lo.nsq);
+            IsoArgs ia{spec[cur], uxi, uyi, nprev, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
                        (long long)Lo.ngroups * H, P};
-            if (int e = hchk(admm_mixed::iso_norm(N, ia, first, s), "k_iso_norm_m")) return e;
+            if (int e = hchk(admm_mixed::iso_norm(N, ia, first, train, s), "k_iso_norm_m")) return e;
             const long long n4 = 2LL * H * W / 4;
             hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, at<float4>(ws, Lo.part),
                                reinterpret_cast<float4*>(nout), Lo.ngroups, n4);
@@ -1573,9 +1599,9 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
         }
         {
             ProfScope ps(0, s);
-            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, nullptr, lam, rho, twW, H, R,
+            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R,
                          rows / R, P, 0};
-            if (int e = hchk(admm_mixed::pass_a(N, pa, d.iso != 0, first, s), "k_pass_a_m")) return e;
+            if (int e = hchk(admm_mixed::pass_a(N, pa, d.iso != 0, first, train, s), "k_pass_a_m")) return e;
         }
         cur = 1 - cur;
         uin = 1 - uin;
@@ -1609,7 +1635,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         return 0;
     }
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
-    if (Lo.mixed && !hist) return run_forward_mixed(d, Lo, xin, lam, rho, out, ws, s);
+    if (Lo.mixed && (!hist || Lo.mixed_train)) return run_forward_mixed(d, Lo, xin, lam, rho, out, ws, hist, s);
     if (Lo.gen) return run_forward_gen(d, Lo, xin, lam, rho, out, ws, hist, s);
     cf* twW = at<cf>(ws, Lo.twW);
     cf* twH = at<cf>(ws, Lo.twH);
@@ -1777,7 +1803,10 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     for (int i = 0; i < 4; ++i) B.abar[i] = take(img);
     B.bbar = take(img);  // per module; summed into gxin at the end
     const long long rows = (long long)G * d.B * d.C * d.H;
-    if (B.f.gen) {  // generic backward: one partial pair per 256-pixel block
+    if (B.f.mixed_train) {  // mixed-radix reverse row pass: strips of R rows (a device-independent rule)
+        B.R = strip_rows_mixed((int)d.H, rows, (int)d.W / 2, 512);
+        B.nstrips = rows / B.R;
+    } else if (B.f.gen) {  // generic backward: one partial pair per 256-pixel block
         B.R = 0;
         B.nstrips = (rows * d.W + 255) / 256;
     } else {
@@ -1914,6 +1943,85 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, c
 
 // ------------------------------------------------------------------ fp64 solves (ADMM_TV_FLAG_F64)
 // The forward of an fp64 solve: run_forward's contract on the generic kernels' double instantiation.
+// training backward at a smooth size (Layout::mixed_train; one module, no PSF gradient): the fused
+// path's reverse sequence (admm_tv_backward) on the mixed transforms -- r^_k = M x^_k by the inference
+// column pass, [iso: Q_{k-1} and its tau^ partial], the reverse row pass; then the scalars, and
+// x^_in = H_t^T b^ through the generic transforms when there is a PSF.
+int run_backward_mixed(const admm_tv_desc& d, const BwdLayout& BL, const float* lam, const float* rho,
+                       const float* gout, const void* hist, float* gxin, float* glam, float* grho, void* ws,
+                       hipStream_t s) {
+    const Layout& Lo = BL.f;
+    const long long P = d.B * d.C;
+    const int H = (int)d.H, W = (int)d.W, N = W / 2, K = d.maxit;
+    const Hist Hs = make_hist(d);
+    const char* hb = static_cast<const char*>(hist);
+    auto ha = [&](int k, int comp) -> const float* {
+        return reinterpret_cast<const float*>(hb + (size_t)(2 * (k - 1) + comp) * Hs.a_slot);
+    };
+    auto hn = [&](int k) -> const float* { return reinterpret_cast<const float*>(hb + Hs.n_off + (size_t)(k - 1) * Hs.n_slot); };
+    auto hchk = [&](hipError_t e, const char* what) {
+        return e == hipSuccess ? 0 : fail(ADMM_TV_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    cf* twW = at<cf>(ws, Lo.twW);
+    cf* twH = at<cf>(ws, Lo.twH);
+    const float* fcM = at<float>(ws, Lo.fcM);
+    cf* spec[2] = {at<cf>(ws, Lo.spec[0]), at<cf>(ws, Lo.spec[1])};
+    float* ab[4] = {at<float>(ws, BL.abar[0]), at<float>(ws, BL.abar[1]), at<float>(ws, BL.abar[2]),
+                    at<float>(ws, BL.abar[3])};
+    float* bbar = (d.kh == 0 && gxin) ? gxin : at<float>(ws, BL.bbar);  // no PSF: x^_in = b^
+    double* part = at<double>(ws, BL.part);
+    double* tpart = at<double>(ws, BL.tpart);
+    float* q = at<float>(ws, BL.q);
+    const long long rows = P * H;
+    if (d.iso) HIPCHK(hipMemsetAsync(tpart, 0, (size_t)K * BL.ntp * sizeof(double), s));
+    if (int e = hchk(admm_mixed::r2c(N, gout, spec[0], twW, rows, s), "k_row_r2c_m")) return e;
+    int cur = 0, ain = 0;
+    for (int k = K; k >= 1; --k) {
+        {
+            ProfScope ps(1, s);
+            if (int e = hchk(admm_mixed::pass_b(H, spec[cur], fcM, twH, N, P, s), "k_pass_b_m")) return e;
+        }
+        const bool lastk = (k == K), firstk = (k == 1);
+        if (d.iso && !firstk) {
+            ProfScope ps(2, s);
+            BwdIsoArgs qa{spec[cur], ab[2 * ain], ab[2 * ain + 1], ha(k - 1, 0), ha(k - 1, 1), rho,
+                          at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg, (long long)Lo.ngroups * H, P};
+            if (int e = hchk(admm_mixed::bwd_iso_q(N, qa, lastk, s), "k_bwd_iso_q_m")) return e;
+            const long long n4 = 2LL * H * W / 4;
+            hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, at<float4>(ws, Lo.part),
+                               reinterpret_cast<float4*>(q), Lo.ngroups, n4);
+            if (int e = launch_check("k_iso_reduce")) return e;
+            // tau^ partial from this rank's Q (N is already global), then Q over every rank's planes
+            hipLaunchKernelGGL(k_iso_tau_partial<float>, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
+                               tpart + (size_t)(K - k) * BL.ntp, 2LL * H * W);
+            if (int e = launch_check("k_iso_tau_partial")) return e;
+            allreduce(d, q, 2ull * H * W, s);
+        }
+        {
+            ProfScope ps(0, s);
+            BwdArgs ba{spec[cur], spec[1 - cur], bbar,
+                       ab[2 * ain], ab[2 * ain + 1], ab[2 * (1 - ain)], ab[2 * (1 - ain) + 1],
+                       ha(k, 0), ha(k, 1),
+                       firstk ? nullptr : ha(k - 1, 0), firstk ? nullptr : ha(k - 1, 1),
+                       (d.iso && !firstk) ? hn(k - 1) : nullptr, q, lam, rho,
+                       part + (size_t)(K - k) * BL.nstrips * 2, twW, H, BL.R, BL.nstrips, P};
+            if (int e = hchk(admm_mixed::bwd_pass_a(N, ba, d.iso != 0, lastk, firstk, s), "k_bwd_pass_a_m")) return e;
+        }
+        cur = 1 - cur;
+        ain = 1 - ain;
+    }
+    if (glam && grho) {
+        hipLaunchKernelGGL(k_bwd_scalars<float>, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, BL.nstrips, 0LL,
+                           d.iso ? tpart : nullptr, BL.ntp, 1, 0, lam, rho, glam, grho);
+        if (int e = launch_check("k_bwd_scalars")) return e;
+    } else if (glam || grho) {
+        return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
+    }
+    if (gxin && d.kh > 0)  // x^_in = H_t^T b^ (the conjugate multiplier, generic transforms)
+        if (int e = gapply<float>(bbar, gxin, spec[0], Lo, ws, d, 2, s)) return e;
+    return 0;
+}
+
 int run_forward_f64(const admm_tv_desc& d, const double* xin, const double* kern, const double* lam,
                     const double* rho, double* out, void* ws, size_t ws_bytes, void* hist, hipStream_t s) {
     const Layout Lo = make_layout(d);
@@ -2069,6 +2177,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     }
     if (!hist || hist_bytes < make_hist(d).total) return fail(ADMM_TV_EWORKSPACE, "history buffer too small");
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
+    if (Lo.mixed_train) return run_backward_mixed(d, BL, lam, rho, gout, hist, gxin, glam, grho, ws, s);
     if (Lo.gen) return run_backward_gen(d, BL, xin, lam, rho, gout, hist, gxin, glam, grho, gkern, ws, s);
     const Hist Hs = make_hist(d);
     char* hb = static_cast<char*>(const_cast<void*>(hist));

@@ -99,8 +99,8 @@ int pass_a_blocks_per_cu(int N) {
     (void)with_row(N, [&](auto n) {
         constexpr int NN = decltype(n)::value;
         using G = MRowG<NN>;
-        if (lds(k_pass_a_m<NN, false, false>, G::lds_bytes()) != hipSuccess) return hipSuccess;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pass_a_m<NN, false, false>, G::NT, G::lds_bytes()) !=
+        if (lds(k_pass_a_m<NN, false, false, false>, G::lds_bytes()) != hipSuccess) return hipSuccess;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pass_a_m<NN, false, false, false>, G::NT, G::lds_bytes()) !=
             hipSuccess)
             nb = 0;
         return hipSuccess;
@@ -138,7 +138,7 @@ hipError_t c2r(int N, const cf* spec, float* img, const cf* twW, long long rows,
     });
 }
 
-hipError_t pass_a(int N, const PassAArgs& a, bool iso, bool first, hipStream_t s) {
+hipError_t pass_a(int N, const PassAArgs& a, bool iso, bool first, bool hist, hipStream_t s) {
     return with_row(N, [&](auto n) {
         constexpr int NN = decltype(n)::value;
         using G = MRowG<NN>;
@@ -149,12 +149,16 @@ hipError_t pass_a(int N, const PassAArgs& a, bool iso, bool first, hipStream_t s
             hipLaunchKernelGGL(kern, grid, blk, l, s, a);
             return hipGetLastError();
         };
-        if (iso) return first ? go(k_pass_a_m<NN, true, true>) : go(k_pass_a_m<NN, true, false>);
-        return first ? go(k_pass_a_m<NN, false, true>) : go(k_pass_a_m<NN, false, false>);
+        if (hist) {
+            if (iso) return first ? go(k_pass_a_m<NN, true, true, true>) : go(k_pass_a_m<NN, true, false, true>);
+            return first ? go(k_pass_a_m<NN, false, true, true>) : go(k_pass_a_m<NN, false, false, true>);
+        }
+        if (iso) return first ? go(k_pass_a_m<NN, true, true, false>) : go(k_pass_a_m<NN, true, false, false>);
+        return first ? go(k_pass_a_m<NN, false, true, false>) : go(k_pass_a_m<NN, false, false, false>);
     });
 }
 
-hipError_t iso_norm(int N, const IsoArgs& a, bool first, hipStream_t s) {
+hipError_t iso_norm(int N, const IsoArgs& a, bool first, bool hist, hipStream_t s) {
     return with_row(N, [&](auto n) {
         constexpr int NN = decltype(n)::value;
         using G = MRowG<NN>;
@@ -165,7 +169,47 @@ hipError_t iso_norm(int N, const IsoArgs& a, bool first, hipStream_t s) {
             hipLaunchKernelGGL(kern, grid, blk, l, s, a);
             return hipGetLastError();
         };
-        return first ? go(k_iso_norm_m<NN, true>) : go(k_iso_norm_m<NN, false>);
+        if (first) return go(k_iso_norm_m<NN, true, false>);
+        return hist ? go(k_iso_norm_m<NN, false, true>) : go(k_iso_norm_m<NN, false, false>);
+    });
+}
+
+hipError_t bwd_pass_a(int N, const BwdArgs& a, bool iso, bool lastk, bool firstk, hipStream_t s) {
+    return with_row(N, [&](auto n) {
+        constexpr int NN = decltype(n)::value;
+        using G = MRowG<NN>;
+        const dim3 grid(row_blocks<NN>(a.nstrips)), blk(G::NT);
+        const size_t l = G::lds_bytes();
+        auto go = [&](auto kern) {
+            if (hipError_t e = lds(kern, l)) return e;
+            hipLaunchKernelGGL(kern, grid, blk, l, s, a);
+            return hipGetLastError();
+        };
+        switch ((iso ? 4 : 0) | (lastk ? 2 : 0) | (firstk ? 1 : 0)) {
+            case 0: return go(k_bwd_pass_a_m<NN, false, false, false>);
+            case 1: return go(k_bwd_pass_a_m<NN, false, false, true>);
+            case 2: return go(k_bwd_pass_a_m<NN, false, true, false>);
+            case 3: return go(k_bwd_pass_a_m<NN, false, true, true>);
+            case 4: return go(k_bwd_pass_a_m<NN, true, false, false>);
+            case 5: return go(k_bwd_pass_a_m<NN, true, false, true>);
+            case 6: return go(k_bwd_pass_a_m<NN, true, true, false>);
+            default: return go(k_bwd_pass_a_m<NN, true, true, true>);
+        }
+    });
+}
+
+hipError_t bwd_iso_q(int N, const BwdIsoArgs& a, bool lastk, hipStream_t s) {
+    return with_row(N, [&](auto n) {
+        constexpr int NN = decltype(n)::value;
+        using G = MRowG<NN>;
+        const dim3 grid(row_blocks<NN>(a.nitems)), blk(G::NT);
+        const size_t l = G::lds_bytes();
+        auto go = [&](auto kern) {
+            if (hipError_t e = lds(kern, l)) return e;
+            hipLaunchKernelGGL(kern, grid, blk, l, s, a);
+            return hipGetLastError();
+        };
+        return lastk ? go(k_bwd_iso_q_m<NN, true>) : go(k_bwd_iso_q_m<NN, false>);
     });
 }
 

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "admm_backward.hpp"
 #include "admm_kernels.hpp"
 
 namespace admm_mixed {
@@ -20,8 +21,12 @@ int pass_a_blocks_per_cu(int N);  // resident 256-thread blocks of the row pass 
 
 hipError_t r2c(int N, const float* img, cf* spec, const cf* twW, long long rows, hipStream_t s);
 hipError_t c2r(int N, const cf* spec, float* img, const cf* twW, long long rows, hipStream_t s);
-hipError_t pass_a(int N, const admm::PassAArgs& a, bool iso, bool first, hipStream_t s);
-hipError_t iso_norm(int N, const admm::IsoArgs& a, bool first, hipStream_t s);
+// hist: the training forward (a_k into the history; admm_kernels.hpp k_pass_a HIST)
+hipError_t pass_a(int N, const admm::PassAArgs& a, bool iso, bool first, bool hist, hipStream_t s);
+hipError_t iso_norm(int N, const admm::IsoArgs& a, bool first, bool hist, hipStream_t s);
+// the training backward's reverse row pass and iso Q pass (admm_backward.hpp, mixed transforms)
+hipError_t bwd_pass_a(int N, const admm::BwdArgs& a, bool iso, bool lastk, bool firstk, hipStream_t s);
+hipError_t bwd_iso_q(int N, const admm::BwdIsoArgs& a, bool lastk, hipStream_t s);
 hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s);
 // fcM: [H][N + 1] then the column-block-packed copy [N / C][H][C] (C = pass_b_cols): H (2N + 1) floats
 hipError_t fc_mixed(const float* fcT, float* fcM, int H, int N, hipStream_t s);

@@ -19,6 +19,7 @@
 // a power-of-two W with a smooth H (or the reverse) runs here too.
 // Inference only (the training forward and backward of these sizes run on the generic kernels).
 #pragma once
+#include "admm_backward.hpp"
 #include "admm_kernels.hpp"
 #include "mixed_fft.hpp"
 
@@ -570,7 +571,9 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
 // occupancy target of the mixed row pass (waves per SIMD): the plans keep <= 9 pixel pairs per lane
 // (wide row groups where a wave would need more), ~150-170 VGPRs: 2 guaranteed, 3 when they fit
 #define PASSA_M_MINW(ep) ((ep) > 9 ? 1 : 2)
-template <int N, bool ISO, bool FIRST>
+// HIST (the training forward): uxi / uyi hold a_{k-1} (u_{k-1} is rebuilt from it with the norms N_{k-1},
+// admm_kernels.hpp prev_u) and a_k is written instead of u_k -- the history the backward reads
+template <int N, bool ISO, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(PassAArgs a) {
     using G = MRowG<N>;
     constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
@@ -605,6 +608,8 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
     cf* uyo = reinterpret_cast<cf*>(a.uyo + poff);
     const cf* nsx = reinterpret_cast<const cf*>(a.nsq);
     const cf* nsy = reinterpret_cast<const cf*>(a.nsq + (size_t)H * W);
+    const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev);
+    const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + (size_t)H * W);
 
     // row g's x in pixel layout (spectrum row -> c2r)
     auto xrow = [&](int g, cf (&x)[Ep]) {
@@ -630,7 +635,8 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
             cf uy[Ep], fy[Ep];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
-                uy[j] = (FIRST || !pa) ? mkc(0.f, 0.f) : ld_pol<kUNT>(&uyi[ro + t + Lp * j]);
+                if constexpr (HIST) uy[j] = pa ? prev_u<ISO, FIRST, true>(uyi, npy, ro + t + Lp * j, tau) : mkc(0.f, 0.f);
+                else uy[j] = (FIRST || !pa) ? mkc(0.f, 0.f) : ld_pol<kUNT>(&uyi[ro + t + Lp * j]);
                 if constexpr (ISO) fy[j] = pa ? nsy[ro + t + Lp * j] : mkc(0.f, 0.f);
             }
 #pragma unroll
@@ -640,7 +646,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
                 const float z0 = shrink_z<ISO>(a0, tau, ISO ? fy[j].x : 0.f);
                 const float z1 = shrink_z<ISO>(a1, tau, ISO ? fy[j].y : 0.f);
                 const float n0 = a0 - z0, n1 = a1 - z1;  // u_y(new)
-                uy[j] = mkc(n0, n1);
+                uy[j] = HIST ? mkc(a0, a1) : mkc(n0, n1);
                 wyc[j] = mkc(z0 - n0, z1 - n1);
             }
             if (rr < R && pst) {
@@ -679,7 +685,8 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
             float xys[Ep], xls[Ep];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
-                ux[j] = (FIRST || !pa) ? mkc(0.f, 0.f) : ld_pol<kUNT>(&uxi[ro + t + Lp * j]);
+                if constexpr (HIST) ux[j] = pa ? prev_u<ISO, FIRST, true>(uxi, npx, ro + t + Lp * j, tau) : mkc(0.f, 0.f);
+                else ux[j] = (FIRST || !pa) ? mkc(0.f, 0.f) : ld_pol<kUNT>(&uxi[ro + t + Lp * j]);
                 if constexpr (ISO) fx[j] = pa ? nsx[ro + t + Lp * j] : mkc(0.f, 0.f);
                 xys[j] = xcur[j].y;
             }
@@ -692,7 +699,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
                 const float z0 = shrink_z<ISO>(a0, tau, ISO ? fx[j].x : 0.f);
                 const float z1 = shrink_z<ISO>(a1, tau, ISO ? fx[j].y : 0.f);
                 const float n0 = a0 - z0, n1 = a1 - z1;
-                ux[j] = mkc(n0, n1);
+                ux[j] = HIST ? mkc(a0, a1) : mkc(n0, n1);
                 wxp[j] = mkc(z0 - n0, z1 - n1);
             }
             if (pst) {
@@ -711,7 +718,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
 // ---------------------------------------------------------------------------------------------
 // iso pass A1 (k_iso_norm): per-pixel partial sums over a group of planes of a_x^2, a_y^2
 // ---------------------------------------------------------------------------------------------
-template <int N, bool FIRST>
+template <int N, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
     using G = MRowG<N>;
     constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
@@ -730,6 +737,9 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
     const int gm = g == 0 ? H - 1 : g - 1;
     auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
     const bool pa = t < Lp, sa = t < Ls;
+    const float tau = HIST ? a.lam[0] / a.rho[0] : 0.f;
+    const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev);
+    const cf* npy = reinterpret_cast<const cf*>(a.nsq_prev + (size_t)H * W);
     cf sx[Ep], sy[Ep];
 #pragma unroll
     for (int j = 0; j < Ep; ++j) sx[j] = sy[j] = mkc(0.f, 0.f);
@@ -755,8 +765,14 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
         RowXfM<N>::template neighbour<-1>(xys, xls, lx, t);
 #pragma unroll
         for (int j = 0; j < Ep; ++j) {
-            const cf ux = (FIRST || !pa) ? mkc(0.f, 0.f) : uxi[ro + t + Lp * j];
-            const cf uy = (FIRST || !pa) ? mkc(0.f, 0.f) : uyi[ro + t + Lp * j];
+            cf ux = (FIRST || !pa) ? mkc(0.f, 0.f) : uxi[ro + t + Lp * j];
+            cf uy = (FIRST || !pa) ? mkc(0.f, 0.f) : uyi[ro + t + Lp * j];
+            if constexpr (HIST && !FIRST) {  // ux / uy hold a_{k-1}: u_{k-1} = a - f(N_{k-1}) a
+                const size_t rn = (size_t)g * N + t + Lp * j;
+                const cf nx = pa ? npx[rn] : mkc(0.f, 0.f), ny = pa ? npy[rn] : mkc(0.f, 0.f);
+                ux = mkc(ux.x - block_factor(nx.x, tau) * ux.x, ux.y - block_factor(nx.y, tau) * ux.y);
+                uy = mkc(uy.x - block_factor(ny.x, tau) * uy.x, uy.y - block_factor(ny.y, tau) * uy.y);
+            }
             const float xl = xls[j];
             const float ax0 = (vc[j].x - xl) + ux.x, ax1 = (vc[j].y - vc[j].x) + ux.y;
             const float ay0 = (vc[j].x - vp[j].x) + uy.x, ay1 = (vc[j].y - vp[j].y) + uy.y;
@@ -773,6 +789,306 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
         for (int j = 0; j < Ep; ++j) {
             px[t + Lp * j] = sx[j];
             py[t + Lp * j] = sy[j];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// training backward at smooth sizes: the reverse row pass and the iso Q pass of admm_backward.hpp
+// (k_bwd_pass_a, k_bwd_iso_q) on the mixed row transforms.  Same algebra (admm_backward.hpp header),
+// same history layout (pixel-order a_k images, the norms N_k), same per-strip fp64 partials; the
+// column side of a reverse step is the inference pass B (M is self-adjoint).  Lanes past the pixel
+// layout (t >= Lp) load nothing, store nothing and add nothing to the partials.
+// ---------------------------------------------------------------------------------------------
+template <int N, bool ISO, bool LASTK, bool FIRSTK>
+__global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_bwd_pass_a_m(BwdArgs a) {
+    using G = MRowG<N>;
+    constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
+    constexpr bool kNT = ADMM_NT_BWD != 0;
+    constexpr bool kSpecNT = kNT && ((ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512));
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, a.twW, W);
+    __syncthreads();
+    const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
+    long long strip = (long long)blockIdx.x * G::SG + sgl;
+    const bool ok = strip < a.nstrips;  // a wide row group past the last strip redoes it without storing
+    if (!G::WIDE && !ok) return;
+    if (!ok) strip = a.nstrips - 1;
+    const int H = a.H, R = a.R;
+    const int spp = H / R;
+    const long long p = strip / spp;
+    const int i0 = (int)(strip % spp) * R;
+    auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
+    const float rho = a.rho[0];
+    const float tau = a.lam[0] / rho;
+    const bool pa = t < Lp, sa = t < Ls;
+    const bool pst = ok && pa, sst = ok && sa;
+
+    const cf* sp = a.sin + (size_t)p * H * N;
+    cf* so = a.sout + (size_t)p * H * N;
+    const size_t poff = (size_t)p * H * W;
+    auto img = [&](const float* base) { return reinterpret_cast<const cf*>(base + poff); };
+    cf* bb = reinterpret_cast<cf*>(a.bbar + poff);
+    const cf* abxi = LASTK ? nullptr : img(a.abx_in);
+    const cf* abyi = LASTK ? nullptr : img(a.aby_in);
+    cf* abxo = FIRSTK ? nullptr : reinterpret_cast<cf*>(a.abx_out + poff);
+    cf* abyo = FIRSTK ? nullptr : reinterpret_cast<cf*>(a.aby_out + poff);
+    const cf* akx = img(a.akx);
+    const cf* aky = img(a.aky);
+    const cf* apx = FIRSTK ? nullptr : img(a.apx);
+    const cf* apy = FIRSTK ? nullptr : img(a.apy);
+    const cf* npx = reinterpret_cast<const cf*>(a.np);
+    const cf* npy = reinterpret_cast<const cf*>(a.np + (size_t)H * W);
+    const cf* qpx = reinterpret_cast<const cf*>(a.qp);
+    const cf* qpy = reinterpret_cast<const cf*>(a.qp + (size_t)H * W);
+    const cf z2 = mkc(0.f, 0.f);
+
+    auto rrow = [&](int g, cf (&x)[Ep]) {  // r^ row g in pixel layout
+        cf v[EM];
+        if (sa) {
+#pragma unroll
+            for (int j = 0; j < Es; ++j) v[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + Ls * j]);
+        }
+        RowXfM<N>::c2r(v, lx, tw, t);
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) x[j] = v[j];
+    };
+    double rho_acc = 0.0, tau_acc = 0.0;
+    cf rprev[Ep], rcur[Ep], abxp[Ep], abyp[Ep];
+    rrow(i0 == 0 ? H - 1 : i0 - 1, rprev);
+    for (int rr = 0; rr <= R; ++rr) {
+        const int g = i0 + rr >= H ? i0 + rr - H : i0 + rr;
+        const size_t ro = (size_t)g * N;
+        rrow(g, rcur);
+
+        // ---- y direction at row g
+        cf abyc[Ep];
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) {
+            const size_t i = ro + t + Lp * j;
+            const float d0 = rcur[j].x - rprev[j].x, d1 = rcur[j].y - rprev[j].y;  // Dy r^
+            cf ap = z2, npv = z2;
+            if constexpr (!FIRSTK) {
+                if (pa) {
+                    ap = ld_pol<kNT>(&apy[i]);
+                    if constexpr (ISO) npv = npy[i];
+                }
+            }
+            const float zp0 = FIRSTK ? 0.f : shrink_z<ISO>(ap.x, tau, npv.x);
+            const float zp1 = FIRSTK ? 0.f : shrink_z<ISO>(ap.y, tau, npv.y);
+            if (rr < R && pa) {
+                // rho^ += Dy r^ . (w_{k-1} - Dy x_k),  w = 2z - a,  Dy x_k = a_k - a_p + z_p
+                const cf ak = ld_pol<kNT>(&aky[i]);
+                const float e0 = (2.f * zp0 - ap.x) - (ak.x - ap.x + zp0);
+                const float e1 = (2.f * zp1 - ap.y) - (ak.y - ap.y + zp1);
+                rho_acc = fma((double)d0, (double)e0, fma((double)d1, (double)e1, rho_acc));
+            }
+            if constexpr (!FIRSTK) {
+                const cf ub = (LASTK || !pa) ? z2 : ld_pol<kNT>(&abyi[i]);
+                const float wb0 = rho * d0, wb1 = rho * d1;
+                const float zb0 = 2.f * wb0 - ub.x, zb1 = 2.f * wb1 - ub.y;
+                cf q = z2;
+                if constexpr (ISO) q = pa ? qpy[i] : z2;
+                abyc[j] = mkc(ub.x - wb0 + shrink_vjp<ISO>(ap.x, zb0, tau, npv.x, q.x),
+                              ub.y - wb1 + shrink_vjp<ISO>(ap.y, zb1, tau, npv.y, q.y));
+                if constexpr (!ISO) {
+                    if (rr < R && pa) tau_acc += (double)soft_dtau(ap.x, zb0, tau) + (double)soft_dtau(ap.y, zb1, tau);
+                }
+            }
+        }
+        if constexpr (!FIRSTK) {
+            if (rr < R && pst) {
+#pragma unroll
+                for (int j = 0; j < Ep; ++j) st_pol<kNT>(&abyo[ro + t + Lp * j], abyc[j]);
+            }
+        }
+        // ---- b^ += r^ (row g)
+        if (rr < R && pst) {
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                cf v = rcur[j];
+                if constexpr (!LASTK) {
+                    const cf o = ld_pol<kNT>(&bb[ro + t + Lp * j]);
+                    v = mkc(o.x + v.x, o.y + v.y);
+                }
+                st_pol<kNT>(&bb[ro + t + Lp * j], v);
+            }
+        }
+        // ---- finalize x^_{k-1} at row g-1: D^T a^ = (a^x[q] - a^x[q+1]) + (a^y[g-1] - a^y[g])
+        if constexpr (!FIRSTK) {
+            if (rr >= 1) {
+                const int gm = g == 0 ? H - 1 : g - 1;
+                const size_t rm = (size_t)gm * N;
+                float axs[Ep], ars[Ep];
+#pragma unroll
+                for (int j = 0; j < Ep; ++j) axs[j] = abxp[j].x;
+                RowXfM<N>::template neighbour<+1>(axs, ars, lx, t);  // a^_x at pixel q1+1
+                cf r[EM];
+#pragma unroll
+                for (int j = 0; j < Ep; ++j)
+                    r[j] = mkc((abxp[j].x - abxp[j].y) + (abyp[j].x - abyc[j].x),
+                               (abxp[j].y - ars[j]) + (abyp[j].y - abyc[j].y));
+                RowXfM<N>::r2c(r, lx, tw, t);
+                if (sst) {
+#pragma unroll
+                    for (int j = 0; j < Es; ++j) st_pol<kNT>(&so[rm + t + Ls * j], r[j]);
+                }
+            }
+        }
+        // ---- x direction at row g
+        if (rr < R) {
+            float rys[Ep], rls[Ep];
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) rys[j] = rcur[j].y;
+            RowXfM<N>::template neighbour<-1>(rys, rls, lx, t);  // r^ at pixel q0-1
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                const size_t i = ro + t + Lp * j;
+                const float d0 = rcur[j].x - rls[j], d1 = rcur[j].y - rcur[j].x;  // Dx r^
+                cf ap = z2, npv = z2;
+                if constexpr (!FIRSTK) {
+                    if (pa) {
+                        ap = ld_pol<kNT>(&apx[i]);
+                        if constexpr (ISO) npv = npx[i];
+                    }
+                }
+                const float zp0 = FIRSTK ? 0.f : shrink_z<ISO>(ap.x, tau, npv.x);
+                const float zp1 = FIRSTK ? 0.f : shrink_z<ISO>(ap.y, tau, npv.y);
+                if (pa) {
+                    const cf ak = ld_pol<kNT>(&akx[i]);
+                    const float e0 = (2.f * zp0 - ap.x) - (ak.x - ap.x + zp0);
+                    const float e1 = (2.f * zp1 - ap.y) - (ak.y - ap.y + zp1);
+                    rho_acc = fma((double)d0, (double)e0, fma((double)d1, (double)e1, rho_acc));
+                }
+                if constexpr (!FIRSTK) {
+                    const cf ub = (LASTK || !pa) ? z2 : ld_pol<kNT>(&abxi[i]);
+                    const float wb0 = rho * d0, wb1 = rho * d1;
+                    const float zb0 = 2.f * wb0 - ub.x, zb1 = 2.f * wb1 - ub.y;
+                    cf q = z2;
+                    if constexpr (ISO) q = pa ? qpx[i] : z2;
+                    abxp[j] = mkc(ub.x - wb0 + shrink_vjp<ISO>(ap.x, zb0, tau, npv.x, q.x),
+                                  ub.y - wb1 + shrink_vjp<ISO>(ap.y, zb1, tau, npv.y, q.y));
+                    if constexpr (!ISO) {
+                        if (pa) tau_acc += (double)soft_dtau(ap.x, zb0, tau) + (double)soft_dtau(ap.y, zb1, tau);
+                    }
+                }
+            }
+            if constexpr (!FIRSTK) {
+                if (pst) {
+#pragma unroll
+                    for (int j = 0; j < Ep; ++j) st_pol<kNT>(&abxo[ro + t + Lp * j], abxp[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) {
+            if constexpr (!FIRSTK) abyp[j] = abyc[j];
+            rprev[j] = rcur[j];
+        }
+    }
+    // per-strip partial sums, fixed order: a butterfly over each wave's lanes of the row group, then
+    // (wide groups) the waves' sums in wave order through the group's LDS buffer
+    constexpr int WL = Lg < 64 ? Lg : 64;
+#pragma unroll
+    for (int o = WL / 2; o >= 1; o >>= 1) {
+        rho_acc += __shfl_xor(rho_acc, o, WL);
+        tau_acc += __shfl_xor(tau_acc, o, WL);
+    }
+    if constexpr (G::WIDE) {
+        double* red = reinterpret_cast<double*>(lx.base);  // the group's exchange buffer, no longer read
+        lds_barrier();
+        if (t % 64 == 0) {
+            red[2 * (t / 64)] = rho_acc;
+            red[2 * (t / 64) + 1] = tau_acc;
+        }
+        lds_barrier();
+        if (t == 0) {
+            rho_acc = red[0];
+            tau_acc = red[1];
+#pragma unroll
+            for (int w = 1; w < Lg / 64; ++w) {
+                rho_acc += red[2 * w];
+                tau_acc += red[2 * w + 1];
+            }
+        }
+    }
+    if (ok && t == 0) {
+        a.part[2 * strip + 0] = rho_acc;
+        a.part[2 * strip + 1] = tau_acc;
+    }
+}
+
+// iso: Q_{k-1} = sum over planes of a_{k-1} z^_{k-1} (k_bwd_iso_q) on the mixed row transforms
+template <int N, bool LASTK>
+__global__ void __launch_bounds__(256) k_bwd_iso_q_m(BwdIsoArgs a) {
+    using G = MRowG<N>;
+    constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    load_tw(tw, a.twW, W);
+    __syncthreads();
+    const int sgl = threadIdx.x / Lg, t = threadIdx.x % Lg;
+    long long item = (long long)blockIdx.x * G::SG + sgl;
+    const bool ok = item < a.nitems;
+    if (!G::WIDE && !ok) return;
+    if (!ok) item = a.nitems - 1;
+    const int H = a.H;
+    const int g = (int)(item % H);
+    const int grp = (int)(item / H);
+    const int gm = g == 0 ? H - 1 : g - 1;
+    auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
+    const bool pa = t < Lp, sa = t < Ls;
+    const float rho = a.rho[0];
+    const cf z2 = mkc(0.f, 0.f);
+    cf qx[Ep], qy[Ep];
+#pragma unroll
+    for (int j = 0; j < Ep; ++j) qx[j] = qy[j] = z2;
+    const int p1 = min(a.P, (grp + 1) * a.ppg);
+    for (int p = grp * a.ppg; p < p1; ++p) {
+        const cf* sp = a.sin + (size_t)p * H * N;
+        cf rp[EM], rc[EM];
+        if (sa) {
+#pragma unroll
+            for (int j = 0; j < Es; ++j) {
+                rp[j] = sp[(size_t)gm * N + t + Ls * j];
+                rc[j] = sp[(size_t)g * N + t + Ls * j];
+            }
+        }
+        RowXfM<N>::c2r(rp, lx, tw, t);
+        RowXfM<N>::c2r(rc, lx, tw, t);
+        const size_t ro = (size_t)p * H * N + (size_t)g * N;
+        const cf* abx = reinterpret_cast<const cf*>(a.abx_in);
+        const cf* aby = reinterpret_cast<const cf*>(a.aby_in);
+        const cf* apx = reinterpret_cast<const cf*>(a.apx);
+        const cf* apy = reinterpret_cast<const cf*>(a.apy);
+        float rys[Ep], rls[Ep];
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) rys[j] = rc[j].y;
+        RowXfM<N>::template neighbour<-1>(rys, rls, lx, t);
+        if (pa) {
+#pragma unroll
+            for (int j = 0; j < Ep; ++j) {
+                const size_t i = ro + t + Lp * j;
+                const cf ubx = LASTK ? z2 : abx[i];
+                const cf uby = LASTK ? z2 : aby[i];
+                const cf ax = apx[i], ay = apy[i];
+                const float zx0 = 2.f * rho * (rc[j].x - rls[j]) - ubx.x, zx1 = 2.f * rho * (rc[j].y - rc[j].x) - ubx.y;
+                const float zy0 = 2.f * rho * (rc[j].x - rp[j].x) - uby.x, zy1 = 2.f * rho * (rc[j].y - rp[j].y) - uby.y;
+                qx[j].x = fmaf(ax.x, zx0, qx[j].x);
+                qx[j].y = fmaf(ax.y, zx1, qx[j].y);
+                qy[j].x = fmaf(ay.x, zy0, qy[j].x);
+                qy[j].y = fmaf(ay.y, zy1, qy[j].y);
+            }
+        }
+    }
+    if (ok && pa) {
+        cf* px = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 0) * H * W) + (size_t)g * N;
+        cf* py = reinterpret_cast<cf*>(a.partial + ((size_t)grp * 2 + 1) * H * W) + (size_t)g * N;
+#pragma unroll
+        for (int j = 0; j < Ep; ++j) {
+            px[t + Lp * j] = qx[j];
+            py[t + Lp * j] = qy[j];
         }
     }
 }
