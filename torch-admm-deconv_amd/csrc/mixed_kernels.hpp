@@ -570,7 +570,11 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
 // ---------------------------------------------------------------------------------------------
 // occupancy target of the mixed row pass (waves per SIMD): the plans keep <= 9 pixel pairs per lane
 // (wide row groups where a wave would need more), ~150-170 VGPRs: 2 guaranteed, 3 when they fit
+#ifdef ADMM_PASSA_M_W  // compile-time A/B knob (tools/build_mixed_variant.sh): one target for every row plan
+#define PASSA_M_MINW(ep) (ADMM_PASSA_M_W)
+#else
 #define PASSA_M_MINW(ep) ((ep) > 9 ? 1 : 2)
+#endif
 // HIST (the training forward): uxi / uyi hold a_{k-1} (u_{k-1} is rebuilt from it with the norms N_{k-1},
 // admm_kernels.hpp prev_u) and a_k is written instead of u_k -- the history the backward reads
 template <int N, bool ISO, bool FIRST, bool HIST>
