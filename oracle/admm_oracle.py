@@ -261,7 +261,7 @@ def solve_fourier(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool = 
 
 
 def solve_fourier_jvp(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: bool, maxit: int,
-                      tx: torch.Tensor, tl: torch.Tensor, tr: torch.Tensor):
+                      tx: torch.Tensor, tl: torch.Tensor, tr: torch.Tensor, progress: Callable | None = None):
     """(y, y_dot): solve_fourier and its directional derivatives along K tangents at once, written out
     (forward mode, O(state) memory: no graph is kept, so the full config-5 shape fits where the fp64
     unrolled graph would need ~100 GB).  tx (K, B, C, H, W) are tangents of xin, tl / tr (K,) of lmbd /
@@ -273,7 +273,9 @@ def solve_fourier_jvp(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: boo
       r = b + rho v,  v = Dx^T w_x + Dy^T w_y       r' = b' + rho' v + rho v'
       x = F^-1 fc F r,  fc = 1/(s2 + rho lap)        x' = F^-1 (fc F r' + fc' F r),  fc' = -fc^2 rho' lap
       a = D x + u,  z = S(a; tau),  tau = lmbd/rho   a' = D x' + u',  z' = S'(a; tau) (a', tau')
-      u = a - z,  w = z - u"""
+      u = a - z,  w = z - u
+
+    progress(it) is called after every iteration (long CPU runs report that they are alive)."""
     B, C, H, W = xin.shape
     dt = xin.dtype
     K = tx.shape[0]
@@ -326,7 +328,7 @@ def solve_fourier_jvp(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: boo
     bs = torch.cat([b.unsqueeze(0), db])
     ux = uy = wx = wy = torch.zeros((K + 1,) + tuple(xin.shape), dtype=dt)
     xs = ux
-    for _ in range(int(maxit)):
+    for step in range(int(maxit)):
         v = dxt(wx) + dyt(wy)                            # v_0 and its tangents
         r = bs + rh * v
         r[1:] += tr * v[0]
@@ -341,6 +343,8 @@ def solve_fourier_jvp(xin: torch.Tensor, lmbd, rho, kern: torch.Tensor, iso: boo
         zy = torch.cat([zy0.unsqueeze(0), dzy])
         ux, uy = ax - zx, ay - zy
         wx, wy = zx - ux, zy - uy
+        if progress is not None:
+            progress(step + 1)
     return xs[0], xs[1:]
 
 

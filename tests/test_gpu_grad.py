@@ -127,7 +127,9 @@ def test_grads_c5_full_shape_forward_mode(cuda_dev):
     # the fp32 parameters' exact values (the HIP solve reads lambda / rho as fp32)
     lam32, rho32 = float(torch.tensor(lam0, dtype=torch.float32)), float(torch.tensor(rho0, dtype=torch.float32))
     y, ydot = solve_fourier_jvp(x64, lam32, rho32, torch.empty(0, dtype=torch.float64),
-                                True, it, tx, torch.tensor([0.0, 1.0, 0.0]), torch.tensor([0.0, 0.0, 1.0]))
+                                True, it, tx, torch.tensor([0.0, 1.0, 0.0]), torch.tensor([0.0, 0.0, 1.0]),
+                                progress=lambda k: k % 10 == 0 and print(f"  fp64 forward-mode oracle: iteration {k}/{it}",
+                                                                         flush=True))
     ref = [torch.dot(v.double().flatten(), ydot[i].flatten()).item() for i in range(3)]
     e_fwd = rel(out, y)
     errs = [abs(h - r) / abs(r) for h, r in zip(hip, ref)]
