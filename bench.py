@@ -533,7 +533,11 @@ def main():
     progress("process group up")
     # rank-local shard of synthetic blurred images, generated directly in HBM
     psf = make_psf(kind, k).to(dev) if k else torch.empty(0, device=dev)
-    x = blurred_batch(B, C, H, W, psf.cpu(), seed=CONFIG_SEED + 2 + 1000 * rank, device=dev)
+    # N > 1: each rank synthesises its shard on the host and copies it in, so the ranks never touch
+    # rocFFT (torch.fft on the device): rehearsed on one GPU under a parent process that had used it,
+    # the ranks' first device FFT stalled (rocFFT's kernel cache); the solve itself does not use rocFFT
+    x = blurred_batch(B, C, H, W, psf.cpu(), seed=CONFIG_SEED + 2 + 1000 * rank,
+                      device="cpu" if world > 1 else dev).to(dev)
     lam = torch.tensor([0.01], device=dev)
     rho = torch.tensor([0.02], device=dev)
     torch.cuda.synchronize()
