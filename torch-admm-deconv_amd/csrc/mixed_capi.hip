@@ -231,16 +231,14 @@ hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long 
         // they change no sizes)
         static const int forced = env_int("ADMM_PASSB_M_ORDER", 0);
         static const int fpack = env_int("ADMM_PASSB_M_FPACK", 1);
-        static const int gp = std::max(1, env_int("ADMM_PASSB_M_GP", 1));  // planes per block
         const int order = forced > 0 ? forced : (HH >= 1024 ? 2 : 1);
         auto go = [&](auto cc) {
             constexpr int CC = decltype(cc)::value;
             using G = MColG<HH, CC>;
             const int colblocks = N / CC;
-            const long long groups = (P + gp - 1) / gp;
             if (hipError_t e = lds(k_pass_b_m<HH, CC>, G::lds_bytes())) return e;
-            hipLaunchKernelGGL((k_pass_b_m<HH, CC>), dim3((unsigned)(groups * colblocks)), dim3(G::NT), G::lds_bytes(), s,
-                               spec, fcM, twH, N, colblocks, order, fpack, gp, P);
+            hipLaunchKernelGGL((k_pass_b_m<HH, CC>), dim3((unsigned)(P * colblocks)), dim3(G::NT), G::lds_bytes(), s,
+                               spec, fcM, twH, N, colblocks, order, fpack);
             return hipGetLastError();
         };
         // the plan's columns per block, or fewer when N is no multiple of them (e.g. W = 1080 beside the

@@ -58,19 +58,11 @@ template <> struct MRow<1024> {  // W = 2048 beside a smooth H: 128 lanes x 8 (2
 // each lane keeps 8 pixel pairs (15 per lane at 64 lanes measured ~320 VGPRs: 1 wave per SIMD).
 // (measured slower for 960: 8 * 3 * 5 * 8, pass A 0.304 -> 0.327 ms, profiles/r04_ab_hd_m960v1.txt; 4-wave
 // groups of 4 pairs per lane as 4 * 15 * 4 * 4)
-#ifndef ADMM_M960_W4  // compile-time A/B: 4-wave row groups, 4 pixel pairs per lane (4 * 15 * 4 * 4 over 240 lanes)
 template <> struct MRow<960> {  // W = 1920 (HD): 960 = 8 * 15 * 8 over 120 of 128 lanes
     static constexpr int Lg = 128, Lp = 120, Ep = 8, Ls = 120, Es = 8;
     using Inv = Sched<8, 15, 8>;
     using Fwd = Sched<8, 15, 8>;
 };
-#else
-template <> struct MRow<960> {
-    static constexpr int Lg = 256, Lp = 240, Ep = 4, Ls = 240, Es = 4;
-    using Inv = Sched<4, 15, 4, 4>;
-    using Fwd = Sched<4, 4, 15, 4>;
-};
-#endif
 template <> struct MRow<1920> {  // W = 3840 (4K UHD): spectra and pixels 240 x 8 (4 waves), 8 * 6 * 5 * 8
     static constexpr int Lg = 256, Lp = 240, Ep = 8, Ls = 240, Es = 8;
     using Inv = Sched<8, 6, 5, 8>;
@@ -495,7 +487,7 @@ static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restri
 template <int H, int CC>
 __global__ void __launch_bounds__((MColG<H, CC>::NT))
 k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g, int N, int colblocks, int order,
-           int fpack, int gp, long long P) {
+           int fpack) {
     using G = MColG<H, CC>;
     constexpr int Lc = G::Lc, Ec = G::Ec, C = G::C, EM = G::EM, NBz = G::NBz, Qz = G::Qz;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -504,13 +496,16 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
     load_tw(tw, twH_g, H);
     const int tid = threadIdx.x;
     const int c = tid % C, t = tid / C;
-    int pg, cb;  // plane group pg: planes pg gp ... (a block runs its column block through them in turn, its
-                 // Wiener factors loaded once)
-    pb_tile(xcd_remap(blockIdx.x, gridDim.x), colblocks, order, true, pg, cb);
+    int p, cb;
+    pb_tile(xcd_remap(blockIdx.x, gridDim.x), colblocks, order, true, p, cb);
     const int col = cb * C + c;
+    const rsrc_t rs = make_rsrc(spec + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
     const int voff = (t * N + col) * (int)sizeof(cf);
     const int sstep = Lc * N * (int)sizeof(cf);
     ColBuf<C> buf{data + c};
+    cf v[EM];
+#pragma unroll
+    for (int j = 0; j < Ec; ++j) v[j] = bload_cf(rs, voff, j * sstep);
     // frequencies in layout(Rz): v[q + Qz k] <-> ky = t + Lc q + NBz k (valid for t + Lc q < NBz)
     float m[EM];
     // the factors of this thread's column: from the column-block-packed copy (k_fc_mixed) or the
@@ -526,17 +521,11 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
                                                     : fcM[(size_t)(vt + NBz * k) * (N + 1) + col]) : 0.f;
         }
     };
-    const long long p0 = (long long)pg * gp, p1 = p0 + gp < P ? p0 + gp : P;
-    for (long long p = p0; p < p1; ++p) {
-    const rsrc_t rs = make_rsrc(spec + (size_t)p * H * N, (unsigned)((size_t)H * N * sizeof(cf)));
-    cf v[EM];
-#pragma unroll
-    for (int j = 0; j < Ec; ++j) v[j] = bload_cf(rs, voff, j * sstep);
-    __syncthreads();  // twiddles in LDS; the previous plane's last reads of buf are done
+    __syncthreads();  // twiddles in LDS
     mfft<H, Lc, EM, -1, 1, 1>(v, buf, tw, t, typename MCol<H>::Fwd{});
     // the factors are loaded after the forward transform (fewer live registers through it) rather than
-    // with the data: HD pass B 0.183 -> 0.160 ms (profiles/r04_ab_hd_latef.txt); once per block
-    if (p == p0) load_m();
+    // with the data: HD pass B 0.183 -> 0.160 ms (profiles/r04_ab_hd_latef.txt)
+    load_m();
     if (cb == 0) {  // block-uniform: column 0 carries (DC, Nyquist) packed -> needs F[H - ky]
         __syncthreads();
 #pragma unroll
@@ -574,7 +563,6 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
     mfft<H, Lc, EM, +1, 1, 1>(v, buf, tw, t, typename MCol<H>::Inv{});
 #pragma unroll
     for (int j = 0; j < Ec; ++j) bstore_cf(rs, voff, j * sstep, v[j]);
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
