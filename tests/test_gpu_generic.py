@@ -76,7 +76,7 @@ def test_g7_odd_size_vs_reference(cuda_dev):
     ((1, 3, 2160, 3840), ("gauss:2", 11), False, 4),       # a 4K UHD frame (2^4 3^3 5 x 2^8 3 5)
     ((2, 1, 12000, 3), None, True, 4),                     # 12,000-point columns in global scratch
     ((1, 1, 5, 13001), ("motion", 5), False, 3),           # a prime line beyond 10,240 (any-prime stage)
-    ((1, 1, 3, 13003), ("motion", 5), False, 3),           # the next prime: past F32_MAX_PRIME, solved in fp64
+    ((1, 1, 5, 13003), ("motion", 5), False, 3),           # the next prime: past F32_MAX_PRIME, solved in fp64
     ((1, 1, 16381, 2), None, False, 2),                    # the largest prime under 2^14, fp64
     ((1, 1, 8, 65521), ("motion", 5), False, 2),           # the largest prime line: fp32 input solved in fp64
     ((1, 1, 65521, 2), None, True, 2),                     #   (eops.deconv.F32_MAX_PRIME), O(n^2) per line
