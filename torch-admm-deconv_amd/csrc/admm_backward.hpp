@@ -81,9 +81,22 @@ __device__ __forceinline__ double soft_dtau(double a, double zb, double tau) {
     return (fabs(a) > tau) ? (a > 0.0 ? -zb : zb) : 0.0;
 }
 
-// Row transform configuration of the reverse passes: the training rows (admm_kernels.hpp TrainCfg)
-template <int N> using BwdCfg = TrainCfg<N>;
-template <int N> using BwdGeom = RowGeomC<N, TrainCfg<N>>;
+// Row transform configuration of the reverse row pass.  Its lanes carry five row states (r^ of two
+// rows, a^_x of the previous row, a^_y of two rows) besides the transform, so at the forward's E values
+// per lane the 256-point rows (W = 512: config 5) needed 229 VGPRs iso -- two waves per SIMD, and the
+// latency-bound pass ran at 0.33 of the HBM peak (SQ: an instruction in flight 26 % of the cycles).
+// 256-point rows run here with 4 values per lane over a full wave (4 * 4 * 4 * 4: one more LDS exchange
+// per transform), which halves the state registers.
+template <int N> struct BwdCfg : RowCfg<N> {};
+template <> struct BwdCfg<256> {
+    static constexpr int E = 4;
+    using S = Sched<4, 4, 4, 4>;
+};
+template <int N> struct BwdGeom {
+    static constexpr int E = BwdCfg<N>::E, L = N / E, W = 2 * N;
+    static constexpr int NT = 256, SG = NT / L;
+    static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * RowBuf::slots(N)); }
+};
 
 // occupancy target of the reverse row pass (waves per SIMD), as PASSA_MINW for the forward:
 // 3 for aniso (measured -2.4 % at C3 size; a few registers spill), 2 for iso, whose extra
@@ -296,8 +309,7 @@ struct BwdIsoArgs {
 
 template <int N, bool LASTK>
 __global__ void __launch_bounds__(256) k_bwd_iso_q(BwdIsoArgs a) {
-    using G = BwdGeom<N>;  // the reverse row pass's row configuration (BwdCfg)
-    using Xf = RowXf<N, BwdCfg<N>>;
+    using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
@@ -324,8 +336,8 @@ __global__ void __launch_bounds__(256) k_bwd_iso_q(BwdIsoArgs a) {
             rp[j] = sp[(size_t)gm * N + t + L * j];
             rc[j] = sp[(size_t)g * N + t + L * j];
         }
-        Xf::c2r(rp, buf, tw, t);
-        Xf::c2r(rc, buf, tw, t);
+        RowXf<N>::c2r(rp, buf, tw, t);
+        RowXf<N>::c2r(rc, buf, tw, t);
         const size_t ro = (size_t)p * H * N + (size_t)g * N;
         const cf* abx = reinterpret_cast<const cf*>(a.abx_in);
         const cf* aby = reinterpret_cast<const cf*>(a.aby_in);

@@ -279,10 +279,8 @@ template <int N> struct RowOps {
         hipLaunchKernelGGL(k_row_pair<N>, dim3(blocks(rows)), dim3(G::NT), 0, s, img, out, rows);
         return launch_check("k_row_pair");
     }
-    template <bool ISO, bool FIRST, bool HIST, bool PL> static void pa(const PassAArgs& a, unsigned, hipStream_t s) {
-        using KG = RowGeomC<N, PassCfg<N, HIST>>;  // the training forward: TrainCfg rows
-        const unsigned nb = (unsigned)((a.nstrips + KG::SG - 1) / KG::SG);
-        hipLaunchKernelGGL((k_pass_a<N, ISO, FIRST, HIST, PL>), dim3(nb), dim3(KG::NT), KG::lds_bytes(), s, a);
+    template <bool ISO, bool FIRST, bool HIST, bool PL> static void pa(const PassAArgs& a, unsigned nb, hipStream_t s) {
+        hipLaunchKernelGGL((k_pass_a<N, ISO, FIRST, HIST, PL>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
     }
     static int pass_a(const PassAArgs& a, bool iso, bool first, bool hist, hipStream_t s, bool pl = false) {
         const unsigned nb = blocks(a.nstrips);
@@ -310,19 +308,12 @@ template <int N> struct RowOps {
     }
     static int iso_norm(const IsoArgs& a, bool first, bool hist, hipStream_t s, bool pl = false) {
         const unsigned nb = blocks(a.nitems);
-        if (hist) {  // the training forward (hist = training; u from the history after the first iteration)
-            using KG = RowGeomC<N, TrainCfg<N>>;
-            const unsigned nt = (unsigned)((a.nitems + KG::SG - 1) / KG::SG);
-            if (first)
-                hipLaunchKernelGGL((k_iso_norm<N, true, false, false, true>), dim3(nt), dim3(KG::NT), KG::lds_bytes(), s, a);
-            else
-                hipLaunchKernelGGL((k_iso_norm<N, false, true, false, true>), dim3(nt), dim3(KG::NT), KG::lds_bytes(), s, a);
-            return launch_check("k_iso_norm");
-        }
         if (first && pl)
             hipLaunchKernelGGL((k_iso_norm<N, true, false, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         else if (first)
             hipLaunchKernelGGL((k_iso_norm<N, true, false, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
+        else if (hist)
+            hipLaunchKernelGGL((k_iso_norm<N, false, true, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         else if (pl)
             hipLaunchKernelGGL((k_iso_norm<N, false, false, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         else
@@ -349,12 +340,11 @@ template <int N> struct RowOps {
         return launch_check("k_bwd_pass_a");
     }
     static int bwd_iso_q(const BwdIsoArgs& a, bool lastk, hipStream_t s) {
-        using BG = BwdGeom<N>;
-        const unsigned nb = (unsigned)((a.nitems + BG::SG - 1) / BG::SG);
+        const unsigned nb = blocks(a.nitems);
         if (lastk)
-            hipLaunchKernelGGL((k_bwd_iso_q<N, true>), dim3(nb), dim3(BG::NT), BG::lds_bytes(), s, a);
+            hipLaunchKernelGGL((k_bwd_iso_q<N, true>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         else
-            hipLaunchKernelGGL((k_bwd_iso_q<N, false>), dim3(nb), dim3(BG::NT), BG::lds_bytes(), s, a);
+            hipLaunchKernelGGL((k_bwd_iso_q<N, false>), dim3(nb), dim3(G::NT), G::lds_bytes(), s, a);
         return launch_check("k_bwd_iso_q");
     }
 };

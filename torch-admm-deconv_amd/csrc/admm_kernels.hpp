@@ -193,26 +193,11 @@ __global__ void k_spectra(const double2* __restrict__ G, const double2* __restri
 // ---------------------------------------------------------------------------
 // row transforms of whole images (one sub-group of L lanes per row)
 // ---------------------------------------------------------------------------
-template <int N, class Cfg = RowCfg<N>> struct RowGeomC {
-    static constexpr int E = Cfg::E, L = N / E, W = 2 * N;
+template <int N> struct RowKernelGeom {
+    static constexpr int E = RowCfg<N>::E, L = N / E, W = 2 * N;
     static constexpr int NT = 256, SG = NT / L;
     static constexpr size_t lds_bytes() { return sizeof(cf) * (W + SG * RowBuf::slots(N)); }
 };
-template <int N> using RowKernelGeom = RowGeomC<N>;
-
-// Row configuration of the training passes (the forward with history, its norm pass and the reverse
-// passes, admm_backward.hpp).  Their lanes carry more row state than inference (the reverse row pass: r^
-// of two rows, a^_x of the previous row, a^_y of two rows besides the transform), so at the inference E
-// values per lane the 256-point rows (W = 512: config 5) needed 229 VGPRs iso -- two waves per SIMD, and
-// the latency-bound reverse pass ran at 0.33 of the HBM peak (SQ: an instruction in flight 26 % of the
-// cycles).  256-point rows run here with 4 values per lane over a full wave (4 * 4 * 4 * 4: one more LDS
-// exchange per transform): reverse row pass 229 -> 149 VGPRs, 0.227 -> 0.153 ms at C5 (0.49 of peak).
-template <int N> struct TrainCfg : RowCfg<N> {};
-template <> struct TrainCfg<256> {
-    static constexpr int E = 4;
-    using S = Sched<4, 4, 4, 4>;
-};
-template <int N, bool TRAIN> using PassCfg = typename std::conditional<TRAIN, TrainCfg<N>, RowCfg<N>>::type;
 
 __device__ __forceinline__ void load_tw(cf* dst, const cf* __restrict__ src, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
@@ -671,9 +656,7 @@ __device__ __forceinline__ cf prev_u(const cf* __restrict__ src, const cf* __res
 template <int N, bool ISO, bool FIRST, bool HIST, bool PL>
 __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
     static_assert(!(PL && HIST), "the training history keeps the pixel-order layout");
-    using Cfg = PassCfg<N, HIST>;  // the training forward: TrainCfg rows
-    using G = RowGeomC<N, Cfg>;
-    using Xf = RowXf<N, Cfg>;
+    using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
     constexpr bool kSpecNT = (ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -719,14 +702,14 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
         const int g = (i0 - 1 + H) & (H - 1);
 #pragma unroll
         for (int j = 0; j < E; ++j) xprev[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + L * j]);
-        Xf::c2r(xprev, buf, tw, t);
+        RowXf<N>::c2r(xprev, buf, tw, t);
     }
     for (int rr = 0; rr <= R; ++rr) {
         const int g = (i0 + rr) & (H - 1);
         const size_t ro = (size_t)g * N;  // row offset in cf units (spectrum and pixel pairs alike)
 #pragma unroll
         for (int j = 0; j < E; ++j) xcur[j] = ld_pol<kSpecNT>(&sp[ro + t + L * j]);
-        Xf::c2r(xcur, buf, tw, t);
+        RowXf<N>::c2r(xcur, buf, tw, t);
 
         // ---- y direction: a_y = x[g] - x[g-1] + u_y; z_y, u_y, w_y of row g
         cf wyc[E];
@@ -783,7 +766,7 @@ __global__ void __launch_bounds__(256, PASSA_MINW(N)) k_pass_a(PassAArgs a) {
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
                 r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
             }
-            Xf::r2c(r, buf, tw, t);
+            RowXf<N>::r2c(r, buf, tw, t);
 #pragma unroll
             for (int j = 0; j < E; ++j) sta(&so[rm + t + L * j], r[j]);
         }
@@ -852,14 +835,10 @@ struct IsoArgs {
     long long ppm;     // planes per module (see PassAArgs)
 };
 
-// TRAIN: the training forward's norm pass (every iteration, the first too): TrainCfg rows, as its pass A
-template <int N, bool FIRST, bool HIST, bool PL, bool TRAIN = HIST>
+template <int N, bool FIRST, bool HIST, bool PL>
 __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
     static_assert(!(PL && HIST), "the training history keeps the pixel-order layout");
-    static_assert(!HIST || TRAIN, "u from the history only in training");
-    using Cfg = PassCfg<N, TRAIN>;
-    using G = RowGeomC<N, Cfg>;
-    using Xf = RowXf<N, Cfg>;
+    using G = RowKernelGeom<N>;
     constexpr int E = G::E, L = G::L, W = G::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
@@ -890,8 +869,8 @@ __global__ void __launch_bounds__(256) k_iso_norm(IsoArgs a) {
             xp[j] = sp[(size_t)gm * N + t + L * j];
             xc[j] = sp[(size_t)g * N + t + L * j];
         }
-        Xf::c2r(xp, buf, tw, t);
-        Xf::c2r(xc, buf, tw, t);
+        RowXf<N>::c2r(xp, buf, tw, t);
+        RowXf<N>::c2r(xc, buf, tw, t);
         const size_t ro = (size_t)p * H * N + (size_t)g * N;  // cf units == pixel pairs
         const size_t rn = (size_t)g * N;                      // norm maps are per pixel, shared by planes
         const cf* uxi = reinterpret_cast<const cf*>(a.uxi);
