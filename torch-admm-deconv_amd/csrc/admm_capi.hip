@@ -108,7 +108,7 @@ bool generic_hw(int64_t H, int64_t W) {
 }
 // smooth sizes on the fused two-pass iteration with mixed-radix register transforms (mixed_kernels.hpp,
 // DESIGN.md §7c): W even with a row plan for W / 2, a column plan for H, not both powers of two (those
-// are supported_hw).  Inference only: the training forward / backward of these sizes stay generic.
+// are supported_hw).  Training too (Layout::mixed_train), except with a PSF gradient or grouped modules.
 // ADMM_MIXED=0 (A/B knob) keeps them on the generic kernels.
 bool mixed_hw(int64_t H, int64_t W) {
     if (supported_hw(H, W) || H < 16 || W < 16 || (W & 1) || H > 4096 || W > 4096) return false;

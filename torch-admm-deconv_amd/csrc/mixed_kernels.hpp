@@ -17,7 +17,8 @@
 //     Rz ... Ec returns them.
 // Power-of-two lengths get the plans of fft_core.hpp's RowCfg (natural layout, same arithmetic), so
 // a power-of-two W with a smooth H (or the reverse) runs here too.
-// Inference only (the training forward and backward of these sizes run on the generic kernels).
+// Training too: the forward with history (HIST variants) and the reverse passes (k_bwd_pass_a_m,
+// k_bwd_iso_q_m, at the end of this file); with a PSF gradient the generic kernels train.
 #pragma once
 #include "admm_backward.hpp"
 #include "admm_kernels.hpp"
