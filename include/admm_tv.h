@@ -105,7 +105,8 @@ const char* admm_tv_build_hash(void);
  *    960, 1080, 1200, 1440, 1536, 2160} or a power of two up to 4096, W/2 even, e.g. 1080x1920,
  *    720x1280, 480x640, 2160x3840, 600x800): admm_tv_forward runs the same fused two-pass iteration
  *    with mixed-radix register transforms (ABI v6), and so do the training forward / backward of
- *    one module without a PSF gradient (those run on the generic kernels, as for 2);
+ *    one module without a PSF gradient (with one, or with grouped modules, they run on the generic
+ *    kernels, as for 2);
  * 2: any other size up to 65,536 points per side, run on the generic kernels (mixed-radix
  *    transforms, per-pixel step; the reference accepts any size, deconv.py:103-106): lines up to
  *    10,240 points transform in the kernels' LDS image, longer ones in a global scratch slot per

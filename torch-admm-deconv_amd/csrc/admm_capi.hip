@@ -712,13 +712,6 @@ std::vector<long long> gen_parts(long long P, int H, int ns) {
     return starts;
 }
 
-// planes per chunk of the aniso inference solve (run_forward): ADMM_CHUNK_PLANES > 0 sets it,
-// 0 (or >= P) solves all planes at once
-long long chunk_planes(int H, int W, long long P) {
-    (void)H; (void)W;
-    const long long c = env_int("ADMM_CHUNK_PLANES", 0);
-    return (c <= 0 || c >= P) ? P : c;
-}
 
 // b = H_t(xin) into `bb` through the FFT passes (scratch: spec)
 int psf_transpose_into(const admm_tv_desc& d, const Layout& Lo, void* ws, const float* xin, float* bb, cf* spec,
@@ -1683,10 +1676,7 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         int e = with_row(N, [&](auto ops) { return decltype(ops)::r2c(bimg, t0, twW, Pm * H, s, pl); });
         if (e) return e;
     }
-    // Planes [p0, p0 + np) through all iterations (ppm: planes per module of that range).  The
-    // aniso inference path solves independent planes, so it may run the iterations chunk by chunk:
-    // a chunk's spectra, u and b (28 B/px) then stay in the 256 MiB Infinity Cache between the
-    // passes instead of streaming through HBM (ADMM_CHUNK_PLANES).
+    // Planes [p0, p0 + np) through all iterations (ppm: planes per module of that range).
     auto solve_planes = [&](long long p0, long long np, long long ppm, hipStream_t st) -> int {
     const size_t so = (size_t)p0 * H * N, io = (size_t)p0 * H * W;  // cf / float offsets
     cf* cspec[2] = {spec[0] + so, spec[1] + so};
@@ -1757,28 +1747,9 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     }
     return 0;
     };
-    const bool indep = !d.iso && !train && G == 1;  // planes independent of each other
-    // two plane halves on two streams (the caller's and a per-thread auxiliary one), so one half's
-    // pass A runs beside the other half's pass B (ADMM_STREAMS)
-    if (indep && P >= 2 && env_int("ADMM_STREAMS", 1) >= 2) {
-        int dev = 0;
-        HIPCHK(hipGetDevice(&dev));
-        hipStream_t s2 = aux_stream(s, dev);
-        if (!s2) return fail(ADMM_TV_EHIP, "auxiliary stream");
-        ForkJoin fj(s, {s2});
-        if (fj.err != hipSuccess) return fail(ADMM_TV_EHIP, std::string("fork: ") + hipGetErrorString(fj.err));
-        const long long h = P / 2;
-        int e = solve_planes(0, h, h, s);
-        if (!e) e = solve_planes(h, P - h, P - h, s2);
-        const hipError_t je = fj.finish();
-        if (e) return e;
-        if (je != hipSuccess) return fail(ADMM_TV_EHIP, std::string("join: ") + hipGetErrorString(je));
-        return 0;
-    }
-    const long long chunk = indep ? chunk_planes(H, W, P) : P;
-    for (long long p0 = 0; p0 < P; p0 += chunk)
-        if (int e = solve_planes(p0, std::min(chunk, P - p0), chunk < P ? std::min(chunk, P - p0) : Pm, s)) return e;
-    return 0;
+    // (measured and removed: plane chunks kept resident in the Infinity Cache through all iterations, and
+    // two plane halves on two streams -- DESIGN.md §9; both no faster at C3)
+    return solve_planes(0, P, Pm, s);
 }
 
 // backward workspace = forward layout + a^ ping-pong (4 images) + b^ + per-iteration partials

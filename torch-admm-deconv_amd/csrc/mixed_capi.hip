@@ -226,18 +226,23 @@ int pass_b_cols(int H, int N) {
 hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s) {
     return with_col(H, [&](auto h) {
         constexpr int HH = decltype(h)::value;
-        // tile order: at H >= 1024 one group of all planes -- the column-block pairs walk every plane before
-        // the next pair, so each XCD (a contiguous range of the launch) keeps its columns' Wiener factors in
-        // its L2 instead of re-reading the whole table per plane: HD pass B 9.5 -> 8.5 B/px (1.19 -> 1.06x its
-        // 8 B/px; profiles/r05_rdreq_hd*.json) at the same time; plane-major below.  A/B knobs
-        // ADMM_PASSB_M_ORDER (planes per group), ADMM_PASSB_M_FPACK (the column-block-packed factors); read
-        // once per process (they change no sizes)
+        // tile order (planes per group of the walk; pb_tile): plane-major below H = 1024; above, groups of
+        // two planes, or -- for blocks of 8+ columns (64-byte row segments) -- one group of all planes: the
+        // column-block pairs walk every plane before the next pair, so each XCD (a contiguous range of the
+        // launch) keeps its columns' Wiener factors in its L2 instead of re-reading the table per plane: HD
+        // pass B 9.5 -> 8.5 B/px (1.19 -> 1.06x its 8 B/px; profiles/r05_rdreq_hd*.json) at the same time;
+        // 4K UHD's 2-column blocks lose 12 % that way (profiles/r05_ab_uhd_passb_order.txt) and keep groups of
+        // two.  A/B knobs ADMM_PASSB_M_ORDER (planes per group), ADMM_PASSB_M_FPACK (the column-block-packed
+        // factors); read once per process (they change no sizes)
         static const int forced = env_int("ADMM_PASSB_M_ORDER", 0);
         static const int fpack = env_int("ADMM_PASSB_M_FPACK", 1);
-        const int order = forced > 0 ? forced : (HH >= 1024 ? (int)std::min<long long>(P, 1 << 30) : 1);
         auto go = [&](auto cc) {
             constexpr int CC = decltype(cc)::value;
             using G = MColG<HH, CC>;
+            const int order = forced > 0 ? forced
+                              : HH < 1024 ? 1
+                              : CC >= 8   ? (int)std::min<long long>(P, 1 << 30)
+                                          : 2;
             const int colblocks = N / CC;
             if (hipError_t e = lds(k_pass_b_m<HH, CC>, G::lds_bytes())) return e;
             hipLaunchKernelGGL((k_pass_b_m<HH, CC>), dim3((unsigned)(P * colblocks)), dim3(G::NT), G::lds_bytes(), s,
