@@ -1,5 +1,5 @@
 """CPU check of every mixed-radix transform plan compiled into the library (csrc/mixed_kernels.hpp
-MRow<N> / MCol<H> specialisations): each schedule is run through an exact-arithmetic simulation of the
+MRow<N> / MRowT<N> / MCol<H> specialisations): each schedule is run through an exact-arithmetic simulation of the
 guarded Stockham stages (csrc/mixed_fft.hpp mstage: butterflies t + L q over L lanes, the lanes past the
 last butterfly idle, registers q + Q k, LDS exchange between stages) and compared with numpy's DFT.
 
@@ -108,15 +108,19 @@ def _natural_out(v, N, lanes, e):
 
 
 ROWS = _plans("MRow")
+TRAIN_ROWS = _plans("MRowT")  # the training backward's row plans
 COLS = _plans("MCol")
 
 
 def test_header_has_the_plans():
     assert {n for n, *_ in ROWS} >= {960, 640, 1920, 2048, 1024, 480, 540, 360, 320, 240, 400, 720, 800, 1280}
+    assert {n for n, *_ in TRAIN_ROWS} >= {240, 360, 400, 480, 540, 640, 720, 800, 960, 1280}
+    assert all(int(v["Ep"]) <= 5 for _, v, *_ in TRAIN_ROWS)
     assert {h for h, *_ in COLS} >= {1080, 2160, 720, 960, 540, 480, 360, 240, 600, 768, 800, 1200, 1440, 1536}
 
 
-@pytest.mark.parametrize("N,vals,fwd,inv", ROWS, ids=[str(p[0]) for p in ROWS])
+@pytest.mark.parametrize("N,vals,fwd,inv", ROWS + TRAIN_ROWS,
+                         ids=[str(p[0]) for p in ROWS] + ["T%d" % p[0] for p in TRAIN_ROWS])
 def test_row_plan_exact(N, vals, fwd, inv):
     Lg, Lp, Ep, Ls, Es = (int(vals[k]) for k in ("Lg", "Lp", "Ep", "Ls", "Es"))
     assert Lp * Ep == N and Ls * Es == N and Lp <= Lg and Ls <= Lg and Lg <= 256

@@ -129,8 +129,65 @@ template <> struct MRow<1280> {  // W = 2560: spectra 160 x 8, pixels 256 x 5 (4
     using Fwd = Sched<5, 8, 4, 8>;
 };
 
-template <int N> struct MRowG {
-    using P = MRow<N>;
+// Row plans of the training backward (the reverse row pass and the iso Q pass): their lanes carry five
+// row states besides the transform (admm_backward.hpp), so these plans keep 3-5 pixel pairs per lane over
+// up to 256 lanes and small transform stages (EM 5-8 values), where the inference plans above keep 8 pairs
+// and up to 15-value stages (tools/mixed_plans.py search with Ep <= 5, each plan simulated on the CPU,
+// tests/test_mixed_plans.py).  Lengths without one use the inference plan.
+template <int N> struct MRowT : MRow<N> {};
+template <> struct MRowT<240> {
+    static constexpr int Lg = 64, Lp = 60, Ep = 4, Ls = 40, Es = 6;
+    using Inv = Sched<6, 2, 5, 4>;
+    using Fwd = Sched<4, 5, 2, 6>;
+};
+template <> struct MRowT<360> {
+    static constexpr int Lg = 128, Lp = 120, Ep = 3, Ls = 60, Es = 6;
+    using Inv = Sched<6, 4, 5, 3>;
+    using Fwd = Sched<3, 5, 4, 6>;
+};
+template <> struct MRowT<400> {
+    static constexpr int Lg = 128, Lp = 100, Ep = 4, Ls = 80, Es = 5;
+    using Inv = Sched<5, 4, 5, 4>;
+    using Fwd = Sched<4, 5, 4, 5>;
+};
+template <> struct MRowT<480> {
+    static constexpr int Lg = 128, Lp = 120, Ep = 4, Ls = 80, Es = 6;
+    using Inv = Sched<6, 4, 5, 4>;
+    using Fwd = Sched<4, 5, 4, 6>;
+};
+template <> struct MRowT<540> {
+    static constexpr int Lg = 128, Lp = 108, Ep = 5, Ls = 90, Es = 6;
+    using Inv = Sched<6, 3, 6, 5>;
+    using Fwd = Sched<5, 6, 3, 6>;
+};
+template <> struct MRowT<640> {
+    static constexpr int Lg = 128, Lp = 128, Ep = 5, Ls = 80, Es = 8;
+    using Inv = Sched<8, 2, 8, 5>;
+    using Fwd = Sched<5, 8, 2, 8>;
+};
+template <> struct MRowT<720> {
+    static constexpr int Lg = 256, Lp = 240, Ep = 3, Ls = 90, Es = 8;
+    using Inv = Sched<8, 5, 6, 3>;
+    using Fwd = Sched<3, 6, 5, 8>;
+};
+template <> struct MRowT<800> {
+    static constexpr int Lg = 256, Lp = 200, Ep = 4, Ls = 100, Es = 8;
+    using Inv = Sched<8, 5, 5, 4>;
+    using Fwd = Sched<4, 5, 5, 8>;
+};
+template <> struct MRowT<960> {
+    static constexpr int Lg = 256, Lp = 240, Ep = 4, Ls = 120, Es = 8;
+    using Inv = Sched<8, 5, 6, 4>;
+    using Fwd = Sched<4, 6, 5, 8>;
+};
+template <> struct MRowT<1280> {
+    static constexpr int Lg = 256, Lp = 256, Ep = 5, Ls = 160, Es = 8;
+    using Inv = Sched<8, 4, 8, 5>;
+    using Fwd = Sched<5, 8, 4, 8>;
+};
+
+template <int N, class PL = MRow<N>> struct MRowG {
+    using P = PL;
     static constexpr int Lg = P::Lg, Lp = P::Lp, Ep = P::Ep, Ls = P::Ls, Es = P::Es, W = 2 * N;
     static constexpr int a = sched_regs<N, Lg>(typename P::Inv{}), b = sched_regs<N, Lg>(typename P::Fwd{});
     static constexpr int EM = a > b ? a : b;
@@ -269,8 +326,8 @@ template <int H, int CC = MCol<H>::C> struct MColG {
 // ---------------------------------------------------------------------------------------------
 // packed real-row transforms over one row group (as RowXf<N>, admm_kernels.hpp, in the plan's layouts)
 // ---------------------------------------------------------------------------------------------
-template <int N> struct RowXfM {
-    using G = MRowG<N>;
+template <int N, class PL = MRow<N>> struct RowXfM {
+    using G = MRowG<N, PL>;
     static constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM;
     static constexpr bool WIDE = G::WIDE;
     static constexpr int SYNC = G::SYNC;
@@ -350,19 +407,19 @@ template <int N> struct RowXfM {
     __device__ __forceinline__ static void c2r(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
         if constexpr (WIDE) {
             combine_lds<true>(v, l, tw, t);
-            mfft<N, Lg, EM, +1, SYNC, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Inv{});
+            mfft<N, Lg, EM, +1, SYNC, 2>(v, RowBuf{l.base}, tw, t, typename PL::Inv{});
         } else {
             combine<true>(v, tw, t);
-            mfft<N, Lg, EM, +1, 0, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Inv{});
+            mfft<N, Lg, EM, +1, 0, 2>(v, RowBuf{l.base}, tw, t, typename PL::Inv{});
         }
     }
     // pixel pairs in layout(Ep) -> packed spectrum (2 rfft) in layout(Es)
     __device__ __forceinline__ static void r2c(cf (&v)[EM], Lds& l, const cf* __restrict__ tw, int t) {
         if constexpr (WIDE) {
-            mfft<N, Lg, EM, -1, SYNC, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Fwd{});
+            mfft<N, Lg, EM, -1, SYNC, 2>(v, RowBuf{l.base}, tw, t, typename PL::Fwd{});
             combine_lds<false>(v, l, tw, t);
         } else {
-            mfft<N, Lg, EM, -1, 0, 2>(v, RowBuf{l.base}, tw, t, typename MRow<N>::Fwd{});
+            mfft<N, Lg, EM, -1, 0, 2>(v, RowBuf{l.base}, tw, t, typename PL::Fwd{});
             combine<false>(v, tw, t);
         }
     }
@@ -798,6 +855,10 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
     }
 }
 
+// occupancy target of the reverse row pass on the training plans (waves per SIMD)
+#ifndef BWD_M_MINW
+#define BWD_M_MINW 2
+#endif
 // ---------------------------------------------------------------------------------------------
 // training backward at smooth sizes: the reverse row pass and the iso Q pass of admm_backward.hpp
 // (k_bwd_pass_a, k_bwd_iso_q) on the mixed row transforms.  Same algebra (admm_backward.hpp header),
@@ -806,8 +867,9 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
 // layout (t >= Lp) load nothing, store nothing and add nothing to the partials.
 // ---------------------------------------------------------------------------------------------
 template <int N, bool ISO, bool LASTK, bool FIRSTK>
-__global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_bwd_pass_a_m(BwdArgs a) {
-    using G = MRowG<N>;
+__global__ void __launch_bounds__(256, BWD_M_MINW) k_bwd_pass_a_m(BwdArgs a) {
+    using G = MRowG<N, MRowT<N>>;
+    using Xf = RowXfM<N, MRowT<N>>;
     constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
     constexpr bool kNT = ADMM_NT_BWD != 0;
     constexpr bool kSpecNT = kNT && ((ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512));
@@ -824,7 +886,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_bwd_pass_a_m
     const int spp = H / R;
     const long long p = strip / spp;
     const int i0 = (int)(strip % spp) * R;
-    auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
+    auto lx = Xf::lds_of(tw + W + sgl * RowBuf::slots(N));
     const float rho = a.rho[0];
     const float tau = a.lam[0] / rho;
     const bool pa = t < Lp, sa = t < Ls;
@@ -855,7 +917,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_bwd_pass_a_m
 #pragma unroll
             for (int j = 0; j < Es; ++j) v[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + Ls * j]);
         }
-        RowXfM<N>::c2r(v, lx, tw, t);
+        Xf::c2r(v, lx, tw, t);
 #pragma unroll
         for (int j = 0; j < Ep; ++j) x[j] = v[j];
     };
@@ -928,13 +990,13 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_bwd_pass_a_m
                 float axs[Ep], ars[Ep];
 #pragma unroll
                 for (int j = 0; j < Ep; ++j) axs[j] = abxp[j].x;
-                RowXfM<N>::template neighbour<+1>(axs, ars, lx, t);  // a^_x at pixel q1+1
+                Xf::template neighbour<+1>(axs, ars, lx, t);  // a^_x at pixel q1+1
                 cf r[EM];
 #pragma unroll
                 for (int j = 0; j < Ep; ++j)
                     r[j] = mkc((abxp[j].x - abxp[j].y) + (abyp[j].x - abyc[j].x),
                                (abxp[j].y - ars[j]) + (abyp[j].y - abyc[j].y));
-                RowXfM<N>::r2c(r, lx, tw, t);
+                Xf::r2c(r, lx, tw, t);
                 if (sst) {
 #pragma unroll
                     for (int j = 0; j < Es; ++j) st_pol<kNT>(&so[rm + t + Ls * j], r[j]);
@@ -946,7 +1008,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_bwd_pass_a_m
             float rys[Ep], rls[Ep];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) rys[j] = rcur[j].y;
-            RowXfM<N>::template neighbour<-1>(rys, rls, lx, t);  // r^ at pixel q0-1
+            Xf::template neighbour<-1>(rys, rls, lx, t);  // r^ at pixel q0-1
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
                 const size_t i = ro + t + Lp * j;
@@ -1027,7 +1089,8 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_bwd_pass_a_m
 // iso: Q_{k-1} = sum over planes of a_{k-1} z^_{k-1} (k_bwd_iso_q) on the mixed row transforms
 template <int N, bool LASTK>
 __global__ void __launch_bounds__(256) k_bwd_iso_q_m(BwdIsoArgs a) {
-    using G = MRowG<N>;
+    using G = MRowG<N, MRowT<N>>;
+    using Xf = RowXfM<N, MRowT<N>>;
     constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
@@ -1042,7 +1105,7 @@ __global__ void __launch_bounds__(256) k_bwd_iso_q_m(BwdIsoArgs a) {
     const int g = (int)(item % H);
     const int grp = (int)(item / H);
     const int gm = g == 0 ? H - 1 : g - 1;
-    auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
+    auto lx = Xf::lds_of(tw + W + sgl * RowBuf::slots(N));
     const bool pa = t < Lp, sa = t < Ls;
     const float rho = a.rho[0];
     const cf z2 = mkc(0.f, 0.f);
@@ -1060,8 +1123,8 @@ __global__ void __launch_bounds__(256) k_bwd_iso_q_m(BwdIsoArgs a) {
                 rc[j] = sp[(size_t)g * N + t + Ls * j];
             }
         }
-        RowXfM<N>::c2r(rp, lx, tw, t);
-        RowXfM<N>::c2r(rc, lx, tw, t);
+        Xf::c2r(rp, lx, tw, t);
+        Xf::c2r(rc, lx, tw, t);
         const size_t ro = (size_t)p * H * N + (size_t)g * N;
         const cf* abx = reinterpret_cast<const cf*>(a.abx_in);
         const cf* aby = reinterpret_cast<const cf*>(a.aby_in);
@@ -1070,7 +1133,7 @@ __global__ void __launch_bounds__(256) k_bwd_iso_q_m(BwdIsoArgs a) {
         float rys[Ep], rls[Ep];
 #pragma unroll
         for (int j = 0; j < Ep; ++j) rys[j] = rc[j].y;
-        RowXfM<N>::template neighbour<-1>(rys, rls, lx, t);
+        Xf::template neighbour<-1>(rys, rls, lx, t);
         if (pa) {
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
