@@ -184,6 +184,9 @@ def _setup_context(ctx, inputs, output):
     x, lam, rho, kern, iso, maxit, psf_grad = inputs
     _, hist = output
     ctx.iso, ctx.maxit, ctx.psf_grad = iso, maxit, psf_grad
+    # hist (uint8) never has a gradient: without this autograd would hand _backward a materialised
+    # zero tensor of the whole history (10 GB at the C5 shape, 1.5 ms of fills per backward)
+    ctx.set_materialize_grads(False)
     # x: read by the native backward only for the PSF gradient (b = H_t(x) path), and by a double
     # backward (admmtor._unrolled rebuilds the iteration from it).  An x that requires grad is saved
     # as itself (the double backward must reach it; autograd's usual version check applies, as for
@@ -204,6 +207,8 @@ def _setup_context(ctx, inputs, output):
 
 
 def _backward(ctx, gout, ghist):
+    if gout is None:  # grads are not materialised (above): no gradient reached the solve's output
+        return (None,) * 7
     x, lam, rho, kern, hist = ctx.saved_tensors
     if ctx.xref is not None and ctx.xref[0]._version == ctx.xref[1]:
         x = ctx.xref[0]  # unmodified since the forward (else x stays empty: no double backward)

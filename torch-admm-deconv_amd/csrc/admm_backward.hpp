@@ -391,6 +391,79 @@ __global__ void k_iso_tau_partial(const T* __restrict__ q, const T* __restrict__
     if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
+// per-iteration sums of one module's partials, in place: block `it` sums the module's strips
+// [soff, soff + spm) of iteration it (and its tau^ partials, iso) in a fixed order and writes the two
+// sums over its first strip's pair, which k_bwd_scalars (spm = 1, no tpart) then adds up over the
+// iterations.  (One block over all K x spm pairs took 1.1 ms at the C5 shape.)
+static __global__ void k_bwd_iter_sums(double* __restrict__ part, long long nstrips, long long spm, long long soff,
+                                       const double* __restrict__ tpart, int ntp, int G, int g) {
+    __shared__ double r1[256], r2[256];
+    const int it = blockIdx.x;
+    double* pp = part + ((size_t)it * nstrips + soff) * 2;
+    double sr = 0.0, st = 0.0;
+    for (long long i = threadIdx.x; i < spm; i += blockDim.x) {
+        sr += pp[2 * i + 0];
+        st += pp[2 * i + 1];
+    }
+    if (tpart) {
+        const double* tp = tpart + ((size_t)it * G + g) * ntp;
+        for (int i = threadIdx.x; i < ntp; i += blockDim.x) st += tp[i];
+    }
+    r1[threadIdx.x] = sr;
+    r2[threadIdx.x] = st;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+            r2[threadIdx.x] += r2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        pp[0] = r1[0];
+        pp[1] = r2[0];
+    }
+}
+
+// iso, fused-path backward: Q = sum of the plane-group partials (k_iso_reduce) and, in the same pass,
+// this block's tau^ partial of k_iso_tau_partial (-Q / (s + eps) where the shrink is active) -- one launch
+// and no re-read of Q and N.  tpart[blockIdx.x]; the launch has (n4 + 255) / 256 blocks = ntp.
+static __global__ void k_iso_reduce_tau(const float4* __restrict__ partial, float4* __restrict__ q, int ngroups,
+                                        long long n4, const float4* __restrict__ n, const float* __restrict__ lam,
+                                        const float* __restrict__ rho, double* __restrict__ tpart) {
+    __shared__ double red[256];
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0.0;
+    if (i < n4) {
+        float4 s = partial[i];
+        for (int g = 1; g < ngroups; ++g) {
+            const float4 v = partial[(size_t)g * n4 + i];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        q[i] = s;
+        const float4 nn = n[i];
+        const float tau = lam[0] / rho[0];
+        auto term = [&](float qv, float nv) {
+            const float sq = sqrtf(nv + eps15<float>()), d = sq + eps15<float>();
+            if (1.f - tau / d > 0.f) acc += (double)(-qv / d);
+        };
+        term(s.x, nn.x);
+        term(s.y, nn.y);
+        term(s.z, nn.z);
+        term(s.w, nn.w);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tpart[blockIdx.x] = red[0];
+}
+
 // final scalars of one module: tau^ = sum of its partials, rho^ = sum + tau^ * (-lam / rho^2),
 // lam^ = tau^ / rho.  part: [K][nstrips][2], the module's strips at [soff, soff + spm) of every
 // iteration; tpart (iso, or null): [K][G][ntp].  Single block, fixed order -> deterministic.

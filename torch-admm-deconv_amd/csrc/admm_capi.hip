@@ -255,6 +255,20 @@ int launch_check(const char* what) {
     return 0;
 }
 
+// lambda / rho gradients of one module from the reverse row pass's per-strip fp64 partials
+// ([K][nstrips][2], the module's strips at [soff, soff + spm)) and, iso, the tau^ partials: per-iteration
+// sums (K blocks, in place), then the sum over the iterations.  Fixed order: deterministic.
+template <class T>
+int bwd_scalars(double* part, int K, long long nstrips, long long spm, long long soff, const double* tpart, int ntp,
+                int G, int g, const T* lam, const T* rho, T* glam, T* grho, hipStream_t s) {
+    if (K < 1) return fail(ADMM_TV_EINVAL, "bwd_scalars: no iterations");
+    hipLaunchKernelGGL(k_bwd_iter_sums, dim3((unsigned)K), dim3(256), 0, s, part, nstrips, spm, soff, tpart, ntp, G, g);
+    if (int e = launch_check("k_bwd_iter_sums")) return e;
+    hipLaunchKernelGGL(k_bwd_scalars<T>, dim3(1), dim3(256), 0, s, (const double*)part, K, nstrips, 1LL, soff,
+                       (const double*)nullptr, ntp, G, g, lam, rho, glam, grho);
+    return launch_check("k_bwd_scalars");
+}
+
 // ------------------------------------------------------------------ row-side ops (templated on N = W/2)
 template <int N> struct RowOps {
     using G = RowKernelGeom<N>;
@@ -1786,7 +1800,9 @@ BwdLayout make_bwd_layout(const admm_tv_desc& d) {
     }
     // the lambda / rho gradient partials are fp64 in every solve (admm_backward.hpp)
     B.part = take((size_t)std::max(d.maxit, 1) * B.nstrips * 2 * sizeof(double));
-    B.ntp = 256;
+    // tau^ partials per iteration and module: one per block of the fused paths' Q reduce (k_iso_reduce_tau,
+    // 1,024 values per block); the generic path's k_iso_tau_partial runs that many blocks too
+    B.ntp = (int)std::max<long long>(1, ((long long)d.H * d.W / 2 + 255) / 256);
     B.tpart = take((size_t)std::max(d.maxit, 1) * G * B.ntp * sizeof(double));  // [K][G][ntp]
     B.q = take(G * 2 * (size_t)d.H * d.W * rs);
     if (d.kh > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) {
@@ -1890,9 +1906,9 @@ int run_backward_gen(const admm_tv_desc& d, const BwdLayout& BL, const T* xin, c
         ain = 1 - ain;
     }
     if (glam && grho) {
-        hipLaunchKernelGGL(k_bwd_scalars<T>, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, BL.nstrips, 0LL,
-                           d.iso ? tpart : nullptr, BL.ntp, 1, 0, lam, rho, glam, grho);
-        if (int e = launch_check("k_bwd_scalars")) return e;
+        if (int e = bwd_scalars<T>(part, K, BL.nstrips, BL.nstrips, 0LL, d.iso ? tpart : nullptr, BL.ntp, 1, 0, lam, rho,
+                                   glam, grho, s))
+            return e;
     } else if (glam || grho) {
         return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
     }
@@ -1959,13 +1975,11 @@ int run_backward_mixed(const admm_tv_desc& d, const BwdLayout& BL, const float* 
                           at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg, (long long)Lo.ngroups * H, P};
             if (int e = hchk(admm_mixed::bwd_iso_q(N, qa, lastk, s), "k_bwd_iso_q_m")) return e;
             const long long n4 = 2LL * H * W / 4;
-            hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, at<float4>(ws, Lo.part),
-                               reinterpret_cast<float4*>(q), Lo.ngroups, n4);
-            if (int e = launch_check("k_iso_reduce")) return e;
-            // tau^ partial from this rank's Q (N is already global), then Q over every rank's planes
-            hipLaunchKernelGGL(k_iso_tau_partial<float>, dim3(BL.ntp), dim3(256), 0, s, q, hn(k - 1), lam, rho,
-                               tpart + (size_t)(K - k) * BL.ntp, 2LL * H * W);
-            if (int e = launch_check("k_iso_tau_partial")) return e;
+            // Q and the tau^ partials from this rank's Q (N is already global), then Q over every rank's planes
+            hipLaunchKernelGGL(k_iso_reduce_tau, dim3((unsigned)BL.ntp), dim3(256), 0, s, at<float4>(ws, Lo.part),
+                               reinterpret_cast<float4*>(q), Lo.ngroups, n4, reinterpret_cast<const float4*>(hn(k - 1)),
+                               lam, rho, tpart + (size_t)(K - k) * BL.ntp);
+            if (int e = launch_check("k_iso_reduce_tau")) return e;
             allreduce(d, q, 2ull * H * W, s);
         }
         {
@@ -1982,9 +1996,9 @@ int run_backward_mixed(const admm_tv_desc& d, const BwdLayout& BL, const float* 
         ain = 1 - ain;
     }
     if (glam && grho) {
-        hipLaunchKernelGGL(k_bwd_scalars<float>, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, BL.nstrips, 0LL,
-                           d.iso ? tpart : nullptr, BL.ntp, 1, 0, lam, rho, glam, grho);
-        if (int e = launch_check("k_bwd_scalars")) return e;
+        if (int e = bwd_scalars<float>(part, K, BL.nstrips, BL.nstrips, 0LL, d.iso ? tpart : nullptr, BL.ntp, 1, 0, lam,
+                                       rho, glam, grho, s))
+            return e;
     } else if (glam || grho) {
         return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
     }
@@ -2200,16 +2214,13 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
             const int gpm = Lo.ngroups / G;
             for (int g = 0; g < G; ++g) {  // per module: Q over its planes, then its tau^ partial
                 float* qg = q + (size_t)g * 2 * H * W;
-                hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                                   at<float4>(ws, Lo.part) + (size_t)g * gpm * n4, reinterpret_cast<float4*>(qg),
-                                   gpm, n4);
-                if ((e = launch_check("k_iso_reduce"))) return e;
-                // tau^ partial from this rank's Q (the norm N is already global): summing the
+                // Q and the tau^ partials from this rank's Q (the norm N is already global): summing the
                 // ranks' lambda/rho gradients then counts every plane once
-                hipLaunchKernelGGL(k_iso_tau_partial<float>, dim3(BL.ntp), dim3(256), 0, s, qg,
-                                   hn(k - 1) + (size_t)g * 2 * H * W, lam + g, rho + g,
-                                   tpart + ((size_t)(K - k) * G + g) * BL.ntp, 2LL * H * W);
-                if ((e = launch_check("k_iso_tau_partial"))) return e;
+                hipLaunchKernelGGL(k_iso_reduce_tau, dim3((unsigned)BL.ntp), dim3(256), 0, s,
+                                   at<float4>(ws, Lo.part) + (size_t)g * gpm * n4, reinterpret_cast<float4*>(qg), gpm, n4,
+                                   reinterpret_cast<const float4*>(hn(k - 1) + (size_t)g * 2 * H * W), lam + g, rho + g,
+                                   tpart + ((size_t)(K - k) * G + g) * BL.ntp);
+                if ((e = launch_check("k_iso_reduce_tau"))) return e;
             }
             allreduce(d, q, (size_t)G * 2 * H * W, s);
         }
@@ -2230,9 +2241,9 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
     if (glam && grho) {
         const long long spm = BL.nstrips / G;  // strips of one module (module-major planes)
         for (int g = 0; g < G; ++g) {
-            hipLaunchKernelGGL(k_bwd_scalars<float>, dim3(1), dim3(256), 0, s, part, K, BL.nstrips, spm, (long long)g * spm,
-                               d.iso ? tpart : nullptr, BL.ntp, G, g, lam + g, rho + g, glam + g, grho + g);
-            if ((e = launch_check("k_bwd_scalars"))) return e;
+            if ((e = bwd_scalars<float>(part, K, BL.nstrips, spm, (long long)g * spm, d.iso ? tpart : nullptr, BL.ntp, G, g,
+                                        lam + g, rho + g, glam + g, grho + g, s)))
+                return e;
         }
     } else if (glam || grho) {
         return fail(ADMM_TV_EINVAL, "glam and grho must be given together");
