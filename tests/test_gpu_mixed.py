@@ -144,9 +144,19 @@ def test_mixed_training_gradients_vs_oracle(cuda_dev, monkeypatch, shape, psf, i
     want = [ref.detach()] + list(torch.autograd.grad(ref, (xr, lr, rr), cot.double()))
     e = [rel(a, b) for a, b in zip(got, want)]
     eg = [rel(a, b) for a, b in zip(gen, want)]
+    # the rho gradient is a sum of large cancelling terms (and, aniso, of shrink masks that one fp32 ulp
+    # can flip): one fp32 evaluation lands 1e-7..3e-4 from fp64 depending on the rounding pattern
+    # (test_gpu_sharded._rho_grad_noise).  Its gate is 1e-4 or, where this input is that sensitive, the
+    # spread the reference formulation's own fp32 evaluation (the oracle in fp32) and the generic
+    # kernels show on it
+    lr32 = torch.tensor([0.03], requires_grad=True)
+    rr32 = torch.tensor([0.05], requires_grad=True)
+    ref32 = solve_fourier(x, lr32, rr32, k if k is not None else torch.empty(0), iso, it)
+    noise32 = rel(torch.autograd.grad(ref32, rr32, cot)[0], want[3])
+    rho_gate = max(1e-4, 3 * noise32, 2 * eg[3])
     print(shape, psf, "iso" if iso else "aniso", it, "mixed (out, x, lam, rho):", ["%.2e" % v for v in e],
-          "generic:", ["%.2e" % v for v in eg])
-    assert e[0] <= TOL_REF64 and max(e[1:]) <= 1e-4
+          "generic:", ["%.2e" % v for v in eg], "oracle fp32 rho: %.2e (rho gate %.2e)" % (noise32, rho_gate))
+    assert e[0] <= TOL_REF64 and max(e[1:3]) <= 1e-4 and e[3] <= rho_gate
     assert not torch.equal(got[1], gen[1])  # the mixed kernels ran, not the generic ones
 
 

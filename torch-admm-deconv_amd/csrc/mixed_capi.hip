@@ -143,36 +143,40 @@ hipError_t c2r(int N, const cf* spec, float* img, const cf* twW, long long rows,
 hipError_t pass_a(int N, const PassAArgs& a, bool iso, bool first, bool hist, hipStream_t s) {
     return with_row(N, [&](auto n) {
         constexpr int NN = decltype(n)::value;
-        using G = MRowG<NN>;
-        const dim3 grid(row_blocks<NN>(a.nstrips)), blk(G::NT);
-        const size_t l = G::lds_bytes();
-        auto go = [&](auto kern) {
+        // the launch geometry of the kernel's row plan (MPlan: the training plans with HIST)
+        auto go = [&](auto kern, auto train) {
+            using G = MRowG<NN, MPlan<NN, decltype(train)::value>>;
+            const size_t l = G::lds_bytes();
             if (hipError_t e = lds(kern, l)) return e;
-            hipLaunchKernelGGL(kern, grid, blk, l, s, a);
+            hipLaunchKernelGGL(kern, dim3(row_blocks<NN, MPlan<NN, decltype(train)::value>>(a.nstrips)), dim3(G::NT), l, s,
+                               a);
             return hipGetLastError();
         };
+        const std::true_type T{};
+        const std::false_type F{};
         if (hist) {
-            if (iso) return first ? go(k_pass_a_m<NN, true, true, true>) : go(k_pass_a_m<NN, true, false, true>);
-            return first ? go(k_pass_a_m<NN, false, true, true>) : go(k_pass_a_m<NN, false, false, true>);
+            if (iso) return first ? go(k_pass_a_m<NN, true, true, true>, T) : go(k_pass_a_m<NN, true, false, true>, T);
+            return first ? go(k_pass_a_m<NN, false, true, true>, T) : go(k_pass_a_m<NN, false, false, true>, T);
         }
-        if (iso) return first ? go(k_pass_a_m<NN, true, true, false>) : go(k_pass_a_m<NN, true, false, false>);
-        return first ? go(k_pass_a_m<NN, false, true, false>) : go(k_pass_a_m<NN, false, false, false>);
+        if (iso) return first ? go(k_pass_a_m<NN, true, true, false>, F) : go(k_pass_a_m<NN, true, false, false>, F);
+        return first ? go(k_pass_a_m<NN, false, true, false>, F) : go(k_pass_a_m<NN, false, false, false>, F);
     });
 }
 
 hipError_t iso_norm(int N, const IsoArgs& a, bool first, bool hist, hipStream_t s) {
     return with_row(N, [&](auto n) {
         constexpr int NN = decltype(n)::value;
-        using G = MRowG<NN>;
-        const dim3 grid(row_blocks<NN>(a.nitems)), blk(G::NT);
-        const size_t l = G::lds_bytes();
-        auto go = [&](auto kern) {
+        auto go = [&](auto kern, auto train) {
+            using G = MRowG<NN, MPlan<NN, decltype(train)::value>>;
+            const size_t l = G::lds_bytes();
             if (hipError_t e = lds(kern, l)) return e;
-            hipLaunchKernelGGL(kern, grid, blk, l, s, a);
+            hipLaunchKernelGGL(kern, dim3(row_blocks<NN, MPlan<NN, decltype(train)::value>>(a.nitems)), dim3(G::NT), l, s,
+                               a);
             return hipGetLastError();
         };
-        if (first) return go(k_iso_norm_m<NN, true, false>);
-        return hist ? go(k_iso_norm_m<NN, false, true>) : go(k_iso_norm_m<NN, false, false>);
+        if (first) return go(k_iso_norm_m<NN, true, false>, std::false_type{});
+        return hist ? go(k_iso_norm_m<NN, false, true>, std::true_type{})
+                    : go(k_iso_norm_m<NN, false, false>, std::false_type{});
     });
 }
 

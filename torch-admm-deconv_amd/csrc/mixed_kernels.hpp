@@ -20,6 +20,8 @@
 // Training too: the forward with history (HIST variants) and the reverse passes (k_bwd_pass_a_m,
 // k_bwd_iso_q_m, at the end of this file); with a PSF gradient the generic kernels train.
 #pragma once
+#include <type_traits>
+
 #include "admm_backward.hpp"
 #include "admm_kernels.hpp"
 #include "mixed_fft.hpp"
@@ -635,9 +637,13 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
 #endif
 // HIST (the training forward): uxi / uyi hold a_{k-1} (u_{k-1} is rebuilt from it with the norms N_{k-1},
 // admm_kernels.hpp prev_u) and a_k is written instead of u_k -- the history the backward reads
+// The training forward (HIST) runs on the training row plans (MRowT, as the reverse passes): the history
+// store and the rebuild of u from a_{k-1} add live state that the inference plans would carry at 256 VGPRs.
+template <int N, bool TRAIN> using MPlan = typename std::conditional<TRAIN, MRowT<N>, MRow<N>>::type;
 template <int N, bool ISO, bool FIRST, bool HIST>
-__global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(PassAArgs a) {
-    using G = MRowG<N>;
+__global__ void __launch_bounds__(256, PASSA_M_MINW((MPlan<N, HIST>::Ep))) k_pass_a_m(PassAArgs a) {
+    using G = MRowG<N, MPlan<N, HIST>>;
+    using Xf = RowXfM<N, MPlan<N, HIST>>;
     constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
     constexpr bool kSpecNT = (ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512);
     constexpr bool kUNT = (ADMM_NT & 16) != 0;
@@ -654,7 +660,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
     const int spp = H / R;
     const long long p = strip / spp;
     const int i0 = (int)(strip % spp) * R;
-    auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
+    auto lx = Xf::lds_of(tw + W + sgl * RowBuf::slots(N));
     const float rho = a.rho[0];
     const float tau = a.lam[0] / rho;
     const bool pa = t < Lp, sa = t < Ls;  // lane holds pixels / spectrum elements
@@ -680,7 +686,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
 #pragma unroll
             for (int j = 0; j < Es; ++j) v[j] = ld_pol<kSpecNT>(&sp[(size_t)g * N + t + Ls * j]);
         }
-        RowXfM<N>::c2r(v, lx, tw, t);
+        Xf::c2r(v, lx, tw, t);
 #pragma unroll
         for (int j = 0; j < Ep; ++j) x[j] = v[j];
     };
@@ -724,7 +730,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
             float wxs[Ep], wrs[Ep];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) wxs[j] = wxp[j].x;
-            RowXfM<N>::template neighbour<+1>(wxs, wrs, lx, t);  // w_x at pixel q1+1
+            Xf::template neighbour<+1>(wxs, wrs, lx, t);  // w_x at pixel q1+1
             cf r[EM];
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
@@ -734,7 +740,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
                 const float v1 = (wxp[j].y - wr) + (wyp[j].y - wyc[j].y);
                 r[j] = mkc(fmaf(rho, v0, bb.x), fmaf(rho, v1, bb.y));
             }
-            RowXfM<N>::r2c(r, lx, tw, t);
+            Xf::r2c(r, lx, tw, t);
             if (sst) {
 #pragma unroll
                 for (int j = 0; j < Es; ++j) sta(&so[rm + t + Ls * j], r[j]);
@@ -752,7 +758,7 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
                 if constexpr (ISO) fx[j] = pa ? nsx[ro + t + Lp * j] : mkc(0.f, 0.f);
                 xys[j] = xcur[j].y;
             }
-            RowXfM<N>::template neighbour<-1>(xys, xls, lx, t);  // x at pixel q0-1
+            Xf::template neighbour<-1>(xys, xls, lx, t);  // x at pixel q0-1
 #pragma unroll
             for (int j = 0; j < Ep; ++j) {
                 const float xl = xls[j];
@@ -782,7 +788,8 @@ __global__ void __launch_bounds__(256, PASSA_M_MINW(MRow<N>::Ep)) k_pass_a_m(Pas
 // ---------------------------------------------------------------------------------------------
 template <int N, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
-    using G = MRowG<N>;
+    using G = MRowG<N, MPlan<N, HIST>>;
+    using Xf = RowXfM<N, MPlan<N, HIST>>;
     constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
@@ -797,7 +804,7 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
     const int g = (int)(item % H);
     const int grp = (int)(item / H);
     const int gm = g == 0 ? H - 1 : g - 1;
-    auto lx = RowXfM<N>::lds_of(tw + W + sgl * RowBuf::slots(N));
+    auto lx = Xf::lds_of(tw + W + sgl * RowBuf::slots(N));
     const bool pa = t < Lp, sa = t < Ls;
     const float tau = HIST ? a.lam[0] / a.rho[0] : 0.f;
     const cf* npx = reinterpret_cast<const cf*>(a.nsq_prev);
@@ -816,15 +823,15 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
                 vc[j] = sp[(size_t)g * N + t + Ls * j];
             }
         }
-        RowXfM<N>::c2r(vp, lx, tw, t);
-        RowXfM<N>::c2r(vc, lx, tw, t);
+        Xf::c2r(vp, lx, tw, t);
+        Xf::c2r(vc, lx, tw, t);
         const size_t ro = (size_t)p * H * N + (size_t)g * N;  // cf units == pixel pairs
         const cf* uxi = reinterpret_cast<const cf*>(a.uxi);
         const cf* uyi = reinterpret_cast<const cf*>(a.uyi);
         float xys[Ep], xls[Ep];
 #pragma unroll
         for (int j = 0; j < Ep; ++j) xys[j] = vc[j].y;
-        RowXfM<N>::template neighbour<-1>(xys, xls, lx, t);
+        Xf::template neighbour<-1>(xys, xls, lx, t);
 #pragma unroll
         for (int j = 0; j < Ep; ++j) {
             cf ux = (FIRST || !pa) ? mkc(0.f, 0.f) : uxi[ro + t + Lp * j];
