@@ -183,8 +183,8 @@ hipError_t iso_norm(int N, const IsoArgs& a, bool first, bool hist, hipStream_t 
 hipError_t bwd_pass_a(int N, const BwdArgs& a, bool iso, bool lastk, bool firstk, hipStream_t s) {
     return with_row(N, [&](auto n) {
         constexpr int NN = decltype(n)::value;
-        using G = MRowG<NN, MRowT<NN>>;  // the training plans
-        const dim3 grid(row_blocks<NN, MRowT<NN>>(a.nstrips)), blk(G::NT);
+        using G = MRowG<NN, BPlan<NN>>;  // the reverse passes' plans
+        const dim3 grid(row_blocks<NN, BPlan<NN>>(a.nstrips)), blk(G::NT);
         const size_t l = G::lds_bytes();
         auto go = [&](auto kern) {
             if (hipError_t e = lds(kern, l)) return e;
@@ -207,8 +207,8 @@ hipError_t bwd_pass_a(int N, const BwdArgs& a, bool iso, bool lastk, bool firstk
 hipError_t bwd_iso_q(int N, const BwdIsoArgs& a, bool lastk, hipStream_t s) {
     return with_row(N, [&](auto n) {
         constexpr int NN = decltype(n)::value;
-        using G = MRowG<NN, MRowT<NN>>;  // the training plans
-        const dim3 grid(row_blocks<NN, MRowT<NN>>(a.nitems)), blk(G::NT);
+        using G = MRowG<NN, BPlan<NN>>;  // the reverse passes' plans
+        const dim3 grid(row_blocks<NN, BPlan<NN>>(a.nitems)), blk(G::NT);
         const size_t l = G::lds_bytes();
         auto go = [&](auto kern) {
             if (hipError_t e = lds(kern, l)) return e;

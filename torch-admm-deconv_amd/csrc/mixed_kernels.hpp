@@ -639,7 +639,19 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
 // admm_kernels.hpp prev_u) and a_k is written instead of u_k -- the history the backward reads
 // The training forward (HIST) runs on the training row plans (MRowT, as the reverse passes): the history
 // store and the rebuild of u from a_{k-1} add live state that the inference plans would carry at 256 VGPRs.
-template <int N, bool TRAIN> using MPlan = typename std::conditional<TRAIN, MRowT<N>, MRow<N>>::type;
+// ... where the training plan keeps the inference plan's row-group width: 640 points (10 8 8 over 128
+// lanes -> 5 pairs per lane) 11.4 -> 6.3 ms per 20 iterations at 720p, while a wider group (960: 2 -> 4
+// waves, 360: 1 -> 2) costs more in exchanges than the registers return (HD 10.1 -> 11.6 ms, 360x720
+// 5.6 -> 6.0 ms; profiles/r05_ab_train_fwd_plans.txt).  Compile-time A/B knob ADMM_TRAIN_FWD_PLAN
+// (tools/build_mixed_variant.sh): 0 = inference plans, 2 = training plans for every length.
+#ifndef ADMM_TRAIN_FWD_PLAN
+#define ADMM_TRAIN_FWD_PLAN 1
+#endif
+template <int N> constexpr bool train_fwd_plan() {
+    return ADMM_TRAIN_FWD_PLAN == 2 || (ADMM_TRAIN_FWD_PLAN == 1 && MRowT<N>::Lg == MRow<N>::Lg);
+}
+template <int N, bool TRAIN>
+using MPlan = typename std::conditional<TRAIN && train_fwd_plan<N>(), MRowT<N>, MRow<N>>::type;
 template <int N, bool ISO, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256, PASSA_M_MINW((MPlan<N, HIST>::Ep))) k_pass_a_m(PassAArgs a) {
     using G = MRowG<N, MPlan<N, HIST>>;
@@ -862,6 +874,20 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
     }
 }
 
+// row plan of the reverse passes: the training plans, except where they would widen the row group to 4
+// waves (960, 720): HD reverse row pass 16.55 -> 15.3 ms per 20 iterations on the inference plan, while
+// 360 points keep the training plan's 2-wave group over the 1-wave inference one (8.97 -> 8.55 ms) and
+// 640 its equal-width one (22.6 -> 15.9 ms; profiles/r05_ab_train_bwd_plans.txt).  A/B knob
+// ADMM_TRAIN_BWD_PLAN: 2 = training plans everywhere, 1 = only at equal group width.
+#ifndef ADMM_TRAIN_BWD_PLAN
+#define ADMM_TRAIN_BWD_PLAN 3
+#endif
+template <int N> constexpr bool train_bwd_plan() {
+    constexpr int a = MRow<N>::Lg, b = MRowT<N>::Lg;
+    return ADMM_TRAIN_BWD_PLAN == 2 || (ADMM_TRAIN_BWD_PLAN == 1 && a == b) ||
+           (ADMM_TRAIN_BWD_PLAN == 3 && (b < 256 || a == 256));
+}
+template <int N> using BPlan = typename std::conditional<train_bwd_plan<N>(), MRowT<N>, MRow<N>>::type;
 // occupancy target of the reverse row pass on the training plans (waves per SIMD)
 #ifndef BWD_M_MINW
 #define BWD_M_MINW 2
@@ -875,8 +901,8 @@ __global__ void __launch_bounds__(256) k_iso_norm_m(IsoArgs a) {
 // ---------------------------------------------------------------------------------------------
 template <int N, bool ISO, bool LASTK, bool FIRSTK>
 __global__ void __launch_bounds__(256, BWD_M_MINW) k_bwd_pass_a_m(BwdArgs a) {
-    using G = MRowG<N, MRowT<N>>;
-    using Xf = RowXfM<N, MRowT<N>>;
+    using G = MRowG<N, BPlan<N>>;
+    using Xf = RowXfM<N, BPlan<N>>;
     constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
     constexpr bool kNT = ADMM_NT_BWD != 0;
     constexpr bool kSpecNT = kNT && ((ADMM_NT & 2) != 0 || ((ADMM_NT & 32) != 0 && N >= 512));
@@ -1096,8 +1122,8 @@ __global__ void __launch_bounds__(256, BWD_M_MINW) k_bwd_pass_a_m(BwdArgs a) {
 // iso: Q_{k-1} = sum over planes of a_{k-1} z^_{k-1} (k_bwd_iso_q) on the mixed row transforms
 template <int N, bool LASTK>
 __global__ void __launch_bounds__(256) k_bwd_iso_q_m(BwdIsoArgs a) {
-    using G = MRowG<N, MRowT<N>>;
-    using Xf = RowXfM<N, MRowT<N>>;
+    using G = MRowG<N, BPlan<N>>;
+    using Xf = RowXfM<N, BPlan<N>>;
     constexpr int Lg = G::Lg, Lp = G::Lp, Ep = G::Ep, Ls = G::Ls, Es = G::Es, EM = G::EM, W = G::W;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
