@@ -636,14 +636,14 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
 #define PASSA_M_MINW(ep) ((ep) > 9 ? 1 : 2)
 #endif
 // HIST (the training forward): uxi / uyi hold a_{k-1} (u_{k-1} is rebuilt from it with the norms N_{k-1},
-// admm_kernels.hpp prev_u) and a_k is written instead of u_k -- the history the backward reads
-// The training forward (HIST) runs on the training row plans (MRowT, as the reverse passes): the history
-// store and the rebuild of u from a_{k-1} add live state that the inference plans would carry at 256 VGPRs.
-// ... where the training plan keeps the inference plan's row-group width: 640 points (10 8 8 over 128
-// lanes -> 5 pairs per lane) 11.4 -> 6.3 ms per 20 iterations at 720p, while a wider group (960: 2 -> 4
-// waves, 360: 1 -> 2) costs more in exchanges than the registers return (HD 10.1 -> 11.6 ms, 360x720
-// 5.6 -> 6.0 ms; profiles/r05_ab_train_fwd_plans.txt).  Compile-time A/B knob ADMM_TRAIN_FWD_PLAN
-// (tools/build_mixed_variant.sh): 0 = inference plans, 2 = training plans for every length.
+// admm_kernels.hpp prev_u) and a_k is written instead of u_k -- the history the backward reads.
+// The history store and the u rebuild add live state that the inference plans carry at up to 256 VGPRs, so
+// the training forward runs on the training row plans (MRowT) where they keep the inference plan's
+// row-group width: 640 points (10 8 8 over 128 lanes -> 5 pairs per lane) 11.4 -> 6.3 ms per 20 iterations
+// at 720p, while a wider group (960: 2 -> 4 waves, 360: 1 -> 2) costs more in exchanges than the registers
+// return (HD 10.1 -> 11.6 ms, 360x720 5.6 -> 6.0 ms; profiles/r05_ab_train_fwd_plans.txt).  Compile-time
+// A/B knob ADMM_TRAIN_FWD_PLAN (tools/build_mixed_variant.sh): 0 = inference plans, 2 = training plans for
+// every length.
 #ifndef ADMM_TRAIN_FWD_PLAN
 #define ADMM_TRAIN_FWD_PLAN 1
 #endif
