@@ -50,3 +50,28 @@ def test_admmdeconv_traces_as_one_graph(iso, kern):
     assert y.shape == x.shape
     y.sum().backward()
     assert x.grad.shape == x.shape
+
+
+def test_history_gradient_is_not_materialised():
+    """The training forward's second output (the uint8 history) never has a gradient; with autograd's
+    default grad materialisation a history-sized zero tensor (10 GB at the C5 shape) was allocated and
+    filled before every backward.  _setup_context turns materialisation off, and _backward returns no
+    gradients when the solve's output gradient is absent."""
+    from admmtor import _ops
+
+    class Ctx:
+        needs_input_grad = (True, True, True, False, False, False, False)
+
+        def set_materialize_grads(self, v):
+            self.materialize = v
+
+        def save_for_backward(self, *t):
+            self.saved = t
+
+    ctx = Ctx()
+    x = torch.rand(1, 1, 8, 8)
+    hist = torch.empty(16, dtype=torch.uint8)
+    _ops._setup_context(ctx, (x, torch.ones(1), torch.ones(1), torch.empty(0), False, 3, False),
+                        (torch.empty_like(x), hist))
+    assert ctx.materialize is False
+    assert _ops._backward(ctx, None, None) == (None,) * 7
