@@ -650,8 +650,16 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
 template <int N> constexpr bool train_fwd_plan() {
     return ADMM_TRAIN_FWD_PLAN == 2 || (ADMM_TRAIN_FWD_PLAN == 1 && MRowT<N>::Lg == MRow<N>::Lg);
 }
+// Inference (TRAIN = false) takes the training plans at equal group width too: 720p pass A (640 points,
+// 10 8 8 -> 5 pairs per lane over the same 128 lanes) 0.327 -> 0.309 ms, 2,130 -> 2,215 it/s
+// (profiles/r05_ab_p720_infer_tplan.txt; 800 and 1280 points follow the same rule).  Compile-time A/B knob
+// ADMM_INFER_TPLAN=0: the inference plans.
+#ifndef ADMM_INFER_TPLAN
+#define ADMM_INFER_TPLAN 1
+#endif
+template <int N> constexpr bool infer_tplan() { return ADMM_INFER_TPLAN != 0 && MRowT<N>::Lg == MRow<N>::Lg; }
 template <int N, bool TRAIN>
-using MPlan = typename std::conditional<TRAIN && train_fwd_plan<N>(), MRowT<N>, MRow<N>>::type;
+using MPlan = typename std::conditional<TRAIN ? train_fwd_plan<N>() : infer_tplan<N>(), MRowT<N>, MRow<N>>::type;
 template <int N, bool ISO, bool FIRST, bool HIST>
 __global__ void __launch_bounds__(256, PASSA_M_MINW((MPlan<N, HIST>::Ep))) k_pass_a_m(PassAArgs a) {
     using G = MRowG<N, MPlan<N, HIST>>;
