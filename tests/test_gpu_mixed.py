@@ -106,6 +106,7 @@ TRAIN_CASES = [
     ((1, 1, 240, 1920), ("motion", 5), False, 6),      # HD rows: a wide row group of 2 waves (960 = 8 15 8)
     ((1, 1, 256, 1280), None, True, 6),                # 720p rows (wide, 640 = 10 8 8) beside power-of-two columns
     # the training row plans (MRowT) at every length where a training kernel takes one (§7c rule)
+    ((1, 1, 128, 640), None, True, 6),                 # 320 (VGA rows): every pass on the 1-wave training plan
     ((1, 2, 128, 960), ("motion", 5), False, 6),       # 480: reverse passes on the 2-wave training plan
     ((1, 1, 128, 1080), None, True, 6),                # 540 (4-column blocks: N = 540)
     ((1, 1, 128, 1600), None, True, 5),                # 800: forward and reverse on the 4-wave training plan

@@ -17,7 +17,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "torch-admm-deconv_amd", "csrc", "mixed_kernels.hpp")
-DEFAULTS = {"ADMM_M960_V": 0, "ADMM_M1080_V": 2, "ADMM_M2160_V": 1, "ADMM_M360_V": 1, "ADMM_MROW_V": 1, "ADMM_MCOL_C": 8}
+DEFAULTS = {"ADMM_TPLAN_320": 1, "ADMM_M960_V": 0, "ADMM_M1080_V": 2, "ADMM_M2160_V": 1, "ADMM_M360_V": 1, "ADMM_MROW_V": 1, "ADMM_MCOL_C": 8}
 
 
 def _preprocess(text):
@@ -114,7 +114,7 @@ COLS = _plans("MCol")
 
 def test_header_has_the_plans():
     assert {n for n, *_ in ROWS} >= {960, 640, 1920, 2048, 1024, 480, 540, 360, 320, 240, 400, 720, 800, 1280}
-    assert {n for n, *_ in TRAIN_ROWS} >= {240, 360, 400, 480, 540, 640, 720, 800, 960, 1280}
+    assert {n for n, *_ in TRAIN_ROWS} >= {240, 320, 360, 400, 480, 540, 640, 720, 800, 960, 1280}
     assert all(int(v["Ep"]) <= 5 for _, v, *_ in TRAIN_ROWS)
     assert {h for h, *_ in COLS} >= {1080, 2160, 720, 960, 540, 480, 360, 240, 600, 768, 800, 1200, 1440, 1536}
 

@@ -142,6 +142,18 @@ template <> struct MRowT<240> {
     using Inv = Sched<6, 2, 5, 4>;
     using Fwd = Sched<4, 5, 2, 6>;
 };
+// 320 points (VGA rows): 5 pairs per lane over the inference plan's 64 lanes, so inference takes it too
+// (infer_tplan): VGA pass A 0.1825 -> 0.1552 ms, 3,800 -> 4,215 it/s (profiles/r05_ab_vga_tplan320.txt)
+#ifndef ADMM_TPLAN_320  // compile-time A/B knob: 0 = no training plan for 320 points (VGA rows)
+#define ADMM_TPLAN_320 1
+#endif
+#if ADMM_TPLAN_320
+template <> struct MRowT<320> {
+    static constexpr int Lg = 64, Lp = 64, Ep = 5, Ls = 40, Es = 8;
+    using Inv = Sched<8, 8, 5>;
+    using Fwd = Sched<5, 8, 8>;
+};
+#endif
 template <> struct MRowT<360> {
     static constexpr int Lg = 128, Lp = 120, Ep = 3, Ls = 60, Es = 6;
     using Inv = Sched<6, 4, 5, 3>;
