@@ -42,17 +42,17 @@ CONFIGS = {
     "c3iso": (64, 3, 1024, 1024, "gauss:3", 21, 50, True,
               "C3 with block (iso) shrinkage, the ADMMDeconv default: batch-64 1024x1024x3, 21x21 PSF, 50 iters"),
     "bsd": (32, 3, 321, 481, "gauss:1.5", 9, 50, False,
-            "generic-size path (row f4): batch-32 481x321x3 (BSD image size), 9x9 Gaussian PSF, aniso, 50 iters"),
+            "BSD image size (row f4): batch-32 481x321x3, 9x9 Gaussian PSF, aniso, 50 iters"),
     "hd": (8, 3, 1080, 1920, "gauss:1.5", 9, 50, False,
-           "generic-size path (row f4): batch-8 1080x1920x3 (HD frame), 9x9 Gaussian PSF, aniso, 50 iters"),
+           "HD frame (row f4): batch-8 1080x1920x3, 9x9 Gaussian PSF, aniso, 50 iters"),
     "uhd": (2, 3, 2160, 3840, "gauss:2", 11, 50, False,
-            "smooth-size path (row f4): batch-2 2160x3840x3 (4K UHD frame), 11x11 Gaussian PSF, aniso, 50 iters"),
+            "4K UHD frame (row f4): batch-2 2160x3840x3, 11x11 Gaussian PSF, aniso, 50 iters"),
     "p720": (16, 3, 720, 1280, "gauss:1.5", 9, 50, False,
-             "smooth-size path (row f4): batch-16 720x1280x3 (720p frame), 9x9 Gaussian PSF, aniso, 50 iters"),
+             "720p frame (row f4): batch-16 720x1280x3, 9x9 Gaussian PSF, aniso, 50 iters"),
     "vga": (32, 3, 480, 640, "gauss:1.5", 9, 50, False,
-            "smooth-size path (row f4): batch-32 480x640x3 (VGA frame), 9x9 Gaussian PSF, aniso, 50 iters"),
+            "VGA frame (row f4): batch-32 480x640x3, 9x9 Gaussian PSF, aniso, 50 iters"),
     "sd": (32, 3, 360, 720, "gauss:1.5", 9, 50, False,
-           "smooth-size path (row f4): batch-32 360x720x3, 9x9 Gaussian PSF, aniso, 50 iters"),
+           "360x720 frame (row f4): batch-32 360x720x3, 9x9 Gaussian PSF, aniso, 50 iters"),
     "c2": (32, 3, 512, 512, "motion", 15, 50, False,
            "C2: batch-32 512x512x3, 15x15 motion PSF, lambda 0.01, rho 0.02, aniso, 50 iters"),
     "c5fwd": (16, 3, 512, 512, "none", 0, 100, True,
@@ -76,6 +76,19 @@ GEN_COL_BYTES = 16
 # r^ spectrum 4, a^_k 8, a_k 8, a_{k-1} 8, b^ 4; writes b^ 4, a^_{k-1} 8, the x^ spectrum 4 = 48;
 # k = K reads no a^ and no b^ (36); k = 1 reads no a_{k-1} and writes no a^ / x^ (28)
 BWD_ROW_BYTES, BWD_ROW_LAST_BYTES, BWD_ROW_FIRST_BYTES = 48, 36, 28
+
+
+def path_of(H, W, iso=False, k=0):
+    """The kernel path an inference solve of this size takes, from the library (admm_tv_path, host-only):
+    "fused", "fused mixed-radix", "fused odd-length" or "generic"."""
+    from admmtor import _native
+    return _native.path(_native.desc(1, 1, H, W, k, iso, 1))
+
+
+def labelled(desc, path):
+    """A workload label names the kernel path it ran on, taken from the library at run time (never
+    written into CONFIGS, where it could go stale)."""
+    return f"{desc} [{path} path]"
 
 
 def parse():
@@ -182,9 +195,9 @@ def generic_extras(dev, no_parity, keys=("bsd", "hd")):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
         npx = B * C * H * W
+        path = path_of(H, W, iso, k)
         e = {"value": maxit / dt, "unit": "iterations/s", "ms_per_step": dt * 1e3, "steps": steps,
-             "us_per_iter_per_Mpx": dt / maxit / (npx / 1e6) * 1e6, "workload": desc,
-             "path": {1: "fused", 3: "fused mixed-radix"}.get(_native.load().admm_tv_supported(H, W), "generic")}
+             "us_per_iter_per_Mpx": dt / maxit / (npx / 1e6) * 1e6, "workload": labelled(desc, path), "path": path}
         if not no_parity:
             from oracle.admm_oracle import rel_l2, solve_fourier
             ref = solve_fourier(x[:1, :1].double().cpu(), 0.01, 0.02, psf.double().cpu(), iso, maxit)
@@ -367,7 +380,10 @@ def run_c5(args, world, rank, dev):
     from admmtor.modelbuild.denoiser import DivergentRestorer
     from admmtor.synth import CONFIG_SEED, clean_images
     B, C, H, W, _, _, maxit, _, desc = CONFIGS["c5"]
+    reduced = (args.c5_batch or args.batch) is not None and (args.c5_batch or args.batch) != B
     B = args.c5_batch or args.batch or B
+    if reduced:  # launch rehearsals only; the line names the reduced workload
+        desc += f" [REDUCED: batch {B} per GPU]"
     deconv = {"kern_size": (), "max_iters": maxit, "iso": True}
     torch.manual_seed(CONFIG_SEED + 5)
     model = DivergentRestorer([2, 8, 32], 3, 3, 86, 86, 8, output_activation=torch.nn.Sigmoid(),
@@ -442,7 +458,7 @@ def run_c5(args, world, rank, dev):
             "steps": K, "warmup": args.warmup, "ms_per_step": T / K * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16 autocast (ADMM solve f32)",
             "data": "synthetic (piecewise-constant shapes + AWGN 0.06, seeded per rank); random-init weights",
-            "config": {"workload": desc, "batch_per_gpu": B, "H": H, "W": W,
+            "config": {"workload": desc, "batch_per_gpu": B, "reduced_batch": reduced, "H": H, "W": W,
                        "branch_checkpointing": not args.c5_no_ckpt,
                        "channels_last": bool(args.c5_channels_last), "conv_benchmark": bool(args.c5_conv_benchmark),
                        "parallelism": f"ddp{world}" if world > 1 else "single"},
@@ -523,6 +539,9 @@ def main():
     B, C, H, W, kind, k, maxit, iso, desc = cfg
 
     from admmtor import _native
+    lib_override = os.environ.get("ADMMTOR_LIB_OVERRIDE")  # A/B tooling (tools/gpu_ab_env.sh) only
+    if lib_override:
+        _native.use_library(lib_override)
     from admmtor.sharded import sharded_fft_admm_tv
     from admmtor.synth import CONFIG_SEED, blurred_batch, make_psf
 
@@ -600,12 +619,14 @@ def main():
     K = args.steps
     lib = _native.load()
     build_hash = lib.admm_tv_build_hash().decode()
-    generic = lib.admm_tv_supported(H, W) == 2
+    path = path_of(H, W, iso, k)
+    generic = path == "generic"
+    odd = path == "fused odd-length"
     # The generic aniso inference solve runs two plane halves on two streams (ADMM_GEN_STREAMS): the
     # event times of its launches overlap and do not add up to kernel durations.  Its roofline then
     # comes from a separate profiling pass of the same solve on one stream (after the timed region;
     # the headline value is the timed region's).
-    two_stream = generic and not iso and P >= 2 and os.environ.get("ADMM_GEN_STREAMS", "2") != "1"
+    two_stream = (generic or odd) and not iso and P >= 2 and os.environ.get("ADMM_GEN_STREAMS", "2") != "1"
     roof_steps, roof_note = K, "HIP events of every launch inside the timed region"
     if two_stream:
         roof_steps = min(K, 5)
@@ -678,7 +699,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (piecewise-constant shapes, circular blur, AWGN 0.01; seeded per rank)",
-            "config": {"workload": desc, "batch_per_gpu": B, "reduced_batch": args.batch is not None, "channels": C, "H": H, "W": W, "psf": f"{kind}/{k}",
+            "config": {"workload": labelled(desc, path), "path": path, "batch_per_gpu": B, "reduced_batch": args.batch is not None, "channels": C, "H": H, "W": W, "psf": f"{kind}/{k}",
                        "maxit": maxit, "iso": iso,
                        "parallelism": (f"shard{world} (batch sharded; RCCL broadcast of PSF/lambda/rho per step and "
                                        "the final all_gather of every step's output inside the timed region, on a "
@@ -688,6 +709,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                          "traffic_source": traffic_src, "build_hash": build_hash, "timing": roof_note,
+                         "library": os.path.relpath(_native.lib_path(), ROOT),
                          "launches": dn, "avg_launch_ms": dms / max(dn, 1),
                          "algorithmic_bytes_per_launch": dbytes / max(dn, 1),
                          "per_kernel": {n: {"ms_total": v[0], "launches": v[1],

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ADMM_TV_ABI_VERSION 6
+#define ADMM_TV_ABI_VERSION 7
 
 enum {
     ADMM_TV_OK = 0,
@@ -107,12 +107,25 @@ const char* admm_tv_build_hash(void);
  *    with mixed-radix register transforms (ABI v6), and so do the training forward / backward of
  *    one module without a PSF gradient (with one, or with grouped modules, they run on the generic
  *    kernels, as for 2);
+ * 4: an odd row length with a fused row pass instance (W = 481 = 13 * 37, the BSD image width, any H up
+ *    to 65,536): admm_tv_forward's aniso solve runs the two-launch iteration -- the generic column pass
+ *    and ONE row pass (inverse rows, step, forward rows; prime-factor transforms in LDS, ABI v7) -- iso
+ *    and the training entry points run on the generic kernels, as for 2;
  * 2: any other size up to 65,536 points per side, run on the generic kernels (mixed-radix
  *    transforms, per-pixel step; the reference accepts any size, deconv.py:103-106): lines up to
  *    10,240 points transform in the kernels' LDS image, longer ones in a global scratch slot per
  *    block (part of the workspace);
  * 0: unsupported. */
 int admm_tv_supported(int64_t H, int64_t W);
+
+/* The kernel path a solve of `desc` takes (train = 0: admm_tv_forward; 1: admm_tv_forward_train and
+ * admm_tv_backward): one of the ADMM_TV_PATH_* codes, or a negative ADMM_TV_E* code for an invalid
+ * descriptor.  Host-only (no device call); tests and benchmarks name the path they measured with it. */
+#define ADMM_TV_PATH_FUSED 1    /* power-of-two two-pass iteration (admm_kernels.hpp) */
+#define ADMM_TV_PATH_GENERIC 2  /* generic kernels: column pass, row inverse, step + row forward */
+#define ADMM_TV_PATH_MIXED 3    /* smooth-size two-pass iteration (mixed_kernels.hpp) */
+#define ADMM_TV_PATH_ODD 4      /* odd-length two-launch iteration (odd_kernels.hpp) */
+int admm_tv_path(const admm_tv_desc* desc, int train);
 
 /* 1 when an fp64 solve (ADMM_TV_FLAG_F64) of (H, W) is supported (up to 65,536 points per side;
  * lines beyond 5,120 points transform in global scratch), 0 otherwise. */

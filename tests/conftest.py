@@ -20,6 +20,12 @@ for p in (ROOT, PKG):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# A/B test runs of a library variant (tools/gpu_ab_variant.sh): the test harness, not the package, reads
+# the override and hands it to admmtor._native.use_library before any native call
+if os.environ.get("ADMMTOR_LIB_OVERRIDE"):
+    from admmtor import _native as _nat
+    _nat.use_library(os.environ["ADMMTOR_LIB_OVERRIDE"])
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (ROCm device); parity tests of the HIP path")

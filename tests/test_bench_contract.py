@@ -87,3 +87,18 @@ def test_gpus_mismatch_exits_before_any_gpu_call():
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 2, p.stderr
     assert p.stdout.strip() == "" and "WORLD_SIZE=2" in p.stderr
+
+
+def test_workload_labels_agree_with_the_path():
+    """No CONFIGS label hard-codes a kernel path (round 5's `hd` label said "generic-size path" while the
+    solve ran on the mixed-radix kernels): the path is appended at run time from the library's own answer
+    for the solve's descriptor (admm_tv_path, a host-only query), so a label always names the path its
+    solve takes."""
+    for name, cfg in bench.CONFIGS.items():
+        B, C, H, W, kind, k, maxit, iso, desc = cfg
+        assert "path" not in desc.lower(), (name, desc)
+        path = bench.path_of(H, W, iso, k)
+        assert bench.labelled(desc, path).endswith(f"[{path} path]")
+    assert bench.path_of(1024, 1024) == "fused" and bench.path_of(1080, 1920) == "fused mixed-radix"
+    assert bench.path_of(15, 17) == "generic" and bench.path_of(321, 481) == "fused odd-length"
+    assert bench.path_of(321, 481, iso=True) == "generic"  # iso keeps the generic kernels there

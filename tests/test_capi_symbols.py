@@ -49,7 +49,7 @@ def test_library_is_gfx950_code():
 def test_host_entry_points():
     from admmtor import _native
     lib = _native.load()
-    assert lib.admm_tv_abi_version() == 6
+    assert lib.admm_tv_abi_version() == 7
     fast, generic = 1, 2
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
     assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 8192), (8, 64), (1, 1), (481, 321))] == [generic] * 5
@@ -212,6 +212,50 @@ def test_environment_reads_are_gated():
     assert all(s in knobs_hpp for s in RUNTIME_SETTINGS)
     integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert all(s in integ for s in RUNTIME_SETTINGS)
+
+
+# environment variables the Python package itself may read (admmtor/**/*.py), each documented in
+# opt-outs to PyTorch's own statistics ops and the double backward's checkpoint
+# segment length.  The library path is not among them: tools and tests pick an A/B variant through
+# _native.use_library(), never the package through the environment.
+PACKAGE_ENV = {"ADMMTOR_CHANPOOL", "ADMMTOR_PLANESTAT", "ADMM_SO_SEGMENT", "ADMM_SO_UNROLLED"}
+
+
+def test_package_environment_reads_are_allowlisted():
+    """Every os.environ / os.getenv read in the package names an allowlisted variable; no other access to
+    the environment (a whole-environment scan, a computed name) exists."""
+    found = set()
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "torch-admm-deconv_amd", "admmtor")):
+        for fn in files:
+            if not fn.endswith(".py"):
+                continue
+            path = os.path.join(dirpath, fn)
+            code = re.sub(r"#[^\n]*", "", open(path).read())
+            for m in re.finditer(r"os\.(environ|getenv)", code):
+                tail = code[m.end():m.end() + 80]
+                name = re.match(r'(?:\.get\(|\[|\()\s*"(\w+)"', tail)
+                assert name, f"{fn}: environment access without a literal name: {tail[:40]!r}"
+                found.add(name.group(1))
+    assert found <= PACKAGE_ENV, found - PACKAGE_ENV
+    integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert all(v in integ for v in found), [v for v in found if v not in integ]
+    assert "ADMMTOR_LIB_OVERRIDE" not in open(os.path.join(ROOT, "torch-admm-deconv_amd", "admmtor",
+                                                            "_native.py")).read()
+
+
+def test_release_load_path_ignores_the_override(monkeypatch):
+    """Setting ADMMTOR_LIB_OVERRIDE changes nothing for the package: a fresh interpreter loads the release
+    library."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path[:0] = [%r]\n"
+            "from admmtor import _native\n"
+            "_native.load()\n"
+            "print(_native.lib_path())\n") % os.path.join(ROOT, "torch-admm-deconv_amd")
+    env = dict(os.environ, ADMMTOR_LIB_OVERRIDE=os.path.join(CSRC, "..", "admmtor", "_lib", "libadmm_tv_ab.so"))
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.strip().endswith(os.path.join("_lib", "libadmm_tv.so"))
 
 
 def test_release_library_ignores_ab_knobs():

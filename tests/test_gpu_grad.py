@@ -282,3 +282,22 @@ def test_psf_gradient_vs_oracle(cuda_dev, iso, it, psf, shape):
             assert e <= max(1e-3, f)
     else:
         assert max(ours) <= 2e-2
+
+
+def test_inference_mode_input_with_learnable_lambda(cuda_dev):
+    """an image produced under torch.inference_mode() (e.g. by an eval pipeline) and then
+    solved with learnable lambda / rho trains: the forward copies the inference tensor instead of reading its
+    (absent) version counter; gradients equal those of the same values as an ordinary tensor."""
+    from admmtor.eops.deconv import fft_admm_tv
+    from admmtor.synth import blurred_batch
+    x0 = blurred_batch(1, 3, 64, 64, torch.empty(0), seed=6).to(cuda_dev)
+    with torch.inference_mode():
+        xi = x0 * 1.0
+    assert xi.is_inference()
+    grads = []
+    for x in (xi, x0.clone()):
+        lam = torch.tensor([0.02], device=cuda_dev, requires_grad=True)
+        rho = torch.tensor([0.05], device=cuda_dev, requires_grad=True)
+        out = fft_admm_tv(x, lam, rho, torch.empty(0, device=cuda_dev), True, 10)
+        grads.append(torch.autograd.grad(out.square().sum(), (lam, rho)))
+    assert all(torch.equal(a, b) for a, b in zip(*grads))

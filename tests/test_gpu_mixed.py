@@ -153,18 +153,21 @@ def test_mixed_training_gradients_vs_oracle(cuda_dev, monkeypatch, shape, psf, i
     eg = [rel(a, b) for a, b in zip(gen, want)]
     # the rho gradient is a sum of large cancelling terms (and, aniso, of shrink masks that one fp32 ulp
     # can flip): one fp32 evaluation lands 1e-7..3e-4 from fp64 depending on the rounding pattern
-    # (test_gpu_sharded._rho_grad_noise).  Its gate is 1e-4 or, where this input is that sensitive, the
-    # spread the reference formulation's own fp32 evaluation (the oracle in fp32) and the generic
-    # kernels show on it
+    # (test_gpu_sharded._rho_grad_noise).  Its gate is 1e-4 or, where this input is that sensitive, 3x the
+    # spread of the reference formulation's own fp32 evaluation on it (the oracle in fp32, on the CPU) --
+    # never a term measured on a HIP path (the generic kernels' error is printed only)
     lr32 = torch.tensor([0.03], requires_grad=True)
     rr32 = torch.tensor([0.05], requires_grad=True)
     ref32 = solve_fourier(x, lr32, rr32, k if k is not None else torch.empty(0), iso, it)
     noise32 = rel(torch.autograd.grad(ref32, rr32, cot)[0], want[3])
-    rho_gate = max(1e-4, 3 * noise32, 2 * eg[3])
+    rho_gate = max(1e-4, 3 * noise32)
     print(shape, psf, "iso" if iso else "aniso", it, "mixed (out, x, lam, rho):", ["%.2e" % v for v in e],
           "generic:", ["%.2e" % v for v in eg], "oracle fp32 rho: %.2e (rho gate %.2e)" % (noise32, rho_gate))
     assert e[0] <= TOL_REF64 and max(e[1:3]) <= 1e-4 and e[3] <= rho_gate
-    assert not torch.equal(got[1], gen[1])  # the mixed kernels ran, not the generic ones
+    # the training solve ran on the mixed kernels: the library's own answer for this descriptor (not an
+    # inference from rounding differences)
+    assert _native.path(_native.desc(*shape, k.shape[-1] if k is not None else 0, iso, it), train=True) \
+        == "fused mixed-radix"
 
 
 def test_mixed_size_psf_gradient_uses_generic_history(cuda_dev):

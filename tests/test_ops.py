@@ -75,3 +75,33 @@ def test_history_gradient_is_not_materialised():
                         (torch.empty_like(x), hist))
     assert ctx.materialize is False
     assert _ops._backward(ctx, None, None) == (None,) * 7
+
+
+def test_inference_tensor_input_is_copied_not_versioned():
+    """An image made under torch.inference_mode() and then solved with a learnable lambda / rho: an inference
+    tensor has no version counter (reading x._version raises), so the forward keeps a private copy of it
+    instead of a versioned reference, and the backward sees that copy."""
+    from admmtor import _ops
+
+    class Ctx:
+        needs_input_grad = (False, True, True, False, False, False, False)
+
+        def set_materialize_grads(self, v):
+            self.materialize = v
+
+        def save_for_backward(self, *t):
+            self.saved = t
+
+    with torch.inference_mode():
+        x = torch.rand(1, 1, 8, 8)
+    assert x.is_inference()
+    ctx = Ctx()
+    _ops._setup_context(ctx, (x, torch.ones(1), torch.ones(1), torch.empty(0), False, 3, False),
+                        (torch.empty_like(x), torch.empty(16, dtype=torch.uint8)))
+    xs = ctx.saved[0]
+    assert ctx.xref is None and not xs.is_inference() and torch.equal(xs, x)
+    # an ordinary tensor is still only referenced (no copy) with its version
+    y = torch.rand(1, 1, 8, 8)
+    _ops._setup_context(ctx, (y, torch.ones(1), torch.ones(1), torch.empty(0), False, 3, False),
+                        (torch.empty_like(y), torch.empty(16, dtype=torch.uint8)))
+    assert ctx.saved[0].numel() == 0 and ctx.xref[0].data_ptr() == y.data_ptr()

@@ -1,6 +1,7 @@
 """In-process tuning sweep of the HIP passes (ADMM_PASSB_C / ADMM_PASSA_R env knobs).
 The knobs are read only by an A/B build of the library (csrc/knobs.hpp): bash tools/build_variant.sh ab,
-then run with ADMMTOR_LIB_OVERRIDE=tools/_variants/ab.so.
+then run with ADMMTOR_LIB_OVERRIDE=tools/_variants/ab.so (read here, by the tool: the package
+itself never reads it; this calls admmtor._native.use_library).
 
 usage: python tools/sweep.py [--config c3] [--steps 3] VAR=v1,v2 [VAR2=...]
 Prints per-kernel average launch time and GB/s (algorithmic bytes) for each setting.
@@ -27,6 +28,8 @@ def main():
     ap.add_argument("knobs", nargs="*")
     a = ap.parse_args()
     from admmtor import _native
+    if os.environ.get("ADMMTOR_LIB_OVERRIDE"):
+        _native.use_library(os.environ["ADMMTOR_LIB_OVERRIDE"])
     from admmtor.eops.deconv import fft_admm_tv
     from admmtor.synth import blurred_batch, make_psf
     B, C, H, W, kind, k, maxit, iso, _ = CONFIGS[a.config]

@@ -12,8 +12,11 @@ import hashlib
 import os
 import threading
 
-_LIB_PATH = os.environ.get("ADMMTOR_LIB_OVERRIDE") or \
-    os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libadmm_tv.so")  # override: tuning A/B only
+# The release library.  The package reads no environment variable to pick another one: tuning tools
+# and A/B test runs call use_library() explicitly before the first native call (tools/sweep.py,
+# tests/conftest.py), so a user's job always loads this file.
+RELEASE_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libadmm_tv.so")
+_LIB_PATH = RELEASE_LIB_PATH
 # the same sources built with -DADMM_AB_BUILD=1 (csrc/knobs.hpp): its A/B knobs follow the environment.
 # Never used by the package itself; tests that compare alternative kernels select it with ab_library().
 AB_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libadmm_tv_ab.so")
@@ -32,6 +35,7 @@ EXPORTED = (
     "admm_tv_build_hash",
     "admm_tv_supported",
     "admm_tv_supported_f64",
+    "admm_tv_path",
     "admm_tv_workspace_size",
     "admm_tv_forward",
     "admm_tv_forward_f64",
@@ -83,7 +87,9 @@ class AdmmTvDesc(ctypes.Structure):
 
 ADMM_TV_FLAG_PSF_GRAD = 1
 ADMM_TV_FLAG_F64 = 2  # fp64 solve: the *_f64 entry points, double arrays
-ABI_VERSION = 6
+ABI_VERSION = 7
+# admm_tv_path codes (include/admm_tv.h)
+PATHS = {1: "fused", 2: "generic", 3: "fused mixed-radix", 4: "fused odd-length"}
 
 
 class NativeError(RuntimeError):
@@ -114,6 +120,17 @@ def source_hash():
 
 def lib_path() -> str:
     return _LIB_PATH
+
+
+def use_library(path: str) -> None:
+    """Tuning and A/B tooling only (tools/sweep.py, tests/conftest.py): load `path` (a variant of the
+    library built from the same sources, e.g. tools/_variants/*.so or the A/B build) instead of the
+    release library.  Must run before the first native call of the process."""
+    global _LIB_PATH
+    with _lock:
+        if _lib is not None and os.path.abspath(path) != os.path.abspath(_LIB_PATH):
+            raise RuntimeError("admmtor: use_library() after the native library was loaded")
+        _LIB_PATH = path
 
 
 def load() -> ctypes.CDLL:
@@ -166,6 +183,8 @@ def _open(path: str) -> ctypes.CDLL:
     L.admm_tv_supported.argtypes = [ctypes.c_int64, ctypes.c_int64]
     L.admm_tv_supported_f64.restype = ctypes.c_int
     L.admm_tv_supported_f64.argtypes = [ctypes.c_int64, ctypes.c_int64]
+    L.admm_tv_path.restype = ctypes.c_int
+    L.admm_tv_path.argtypes = [dp, ctypes.c_int]
     L.admm_tv_workspace_size.restype = ctypes.c_int
     L.admm_tv_workspace_size.argtypes = [dp, ctypes.POINTER(sz)]
     for f in ("admm_tv_forward", "admm_tv_forward_f64"):
@@ -250,6 +269,15 @@ def backward_workspace_size(d: AdmmTvDesc) -> int:
     n = ctypes.c_size_t(0)
     check(load().admm_tv_backward_workspace_size(ctypes.byref(d), ctypes.byref(n)))
     return int(n.value)
+
+
+def path(d: AdmmTvDesc, train: bool = False) -> str:
+    """The kernel path a solve of descriptor `d` takes (admm_tv_path): "fused", "generic",
+    "fused mixed-radix" or "fused odd-length"."""
+    code = load().admm_tv_path(ctypes.byref(d), 1 if train else 0)
+    if code < 0:
+        check(code)
+    return PATHS[code]
 
 
 def supported(H: int, W: int, f64: bool = False) -> bool:

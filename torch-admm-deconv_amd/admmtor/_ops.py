@@ -195,10 +195,12 @@ def _setup_context(ctx, inputs, output):
     # PSF gradient a private copy is kept (one image next to the 2 K images of history); otherwise x
     # is only referenced with its version, the first-order backward does not read it, and a double
     # backward after such a modification raises instead of differentiating the wrong input.
+    # An inference tensor (made under torch.inference_mode) tracks no version counter, so it cannot be
+    # referenced with one: it gets the private copy too.
     ctx.xref = None
     if x.requires_grad:
         xs = x
-    elif psf_grad:
+    elif psf_grad or x.is_inference():
         xs = x.detach().clone()
     else:
         xs = x.new_empty(0)

@@ -17,6 +17,8 @@
 #include "gcol_mm.hpp"
 #include "knobs.hpp"
 #include "mixed_capi.hpp"
+#include "odd_capi.hpp"
+#include "odd_kernels.hpp"
 #include "admm_tv.h"
 
 using namespace admm;
@@ -115,6 +117,13 @@ bool mixed_hw(int64_t H, int64_t W) {
     if (!admm_mixed::row_ok((int)(W / 2)) || !admm_mixed::col_ok((int)H)) return false;
     return (W / 2) % admm_mixed::col_cols((int)H) == 0 && env_int("ADMM_MIXED", 1) != 0;
 }
+// odd row lengths with a fused row pass instance (odd_kernels.hpp; BSD's W = 481 = 13 * 37): the
+// aniso inference solve runs the two-launch iteration -- the generic column pass, then ONE row pass
+// (inverse rows, step, forward rows) -- instead of the generic three.  iso and training keep the generic
+// kernels.  ADMM_ODD=0 (A/B knob) keeps every solve on them.
+bool odd_hw(int64_t H, int64_t W) {
+    return generic_hw(H, W) && !mixed_hw(H, W) && admm_odd::row_ok((int)W) && env_int("ADMM_ODD", 1) != 0;
+}
 // fp64 solves (ADMM_TV_FLAG_F64) run on the generic kernels' double instantiation at every size
 bool is_f64(const admm_tv_desc& d) { return (d.flags & ADMM_TV_FLAG_F64) != 0; }
 bool f64_hw(int64_t H, int64_t W) {
@@ -150,6 +159,9 @@ struct Layout {
     // history is the generic path's)
     bool mixed, mixed_train;
     size_t fcM;
+    // fused odd-length row pass (odd_hw, aniso inference): the second half-spectrum buffer of its ping-pong
+    bool odd;
+    size_t spec2;
     size_t rimg;  // generic path: spec[0] = half spectra [P][H][W/2+1], spec[1] = x image, rimg = r image
     size_t gscr;  // generic path, lines beyond the LDS image: the transform blocks' scratch slots
     int ngroups, ppg;
@@ -182,6 +194,7 @@ Layout make_layout(const admm_tv_desc& d) {
     }
     L.mixed = L.gen && !f64 && G == 1 && mixed_hw(d.H, d.W);
     L.mixed_train = L.mixed && !(k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD));
+    L.odd = L.gen && !f64 && G == 1 && !d.iso && odd_hw(d.H, d.W);
     L.ldw = (int)(N + 1);
     if (L.gen && !f64 && L.mm.ok && L.mmr.ok && env_int("ADMM_GEN_PITCH", 1)) L.ldw = (int)((N + 1 + 15) / 16 * 16);
     L.spec[0] = take(L.gen ? P * H * (size_t)L.ldw * csz : img);
@@ -204,6 +217,7 @@ Layout make_layout(const admm_tv_desc& d) {
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
     L.gscr = L.gen ? take(glb_scratch((int)H, (int)W, (long long)P, f64)) : 0;
     L.fcM = L.mixed ? take((2 * N + 1) * H * sizeof(float)) : 0;  // [H][N + 1] + packed copy, k_fc_mixed
+    L.spec2 = L.odd ? take(P * H * (size_t)L.ldw * csz) : 0;
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
         // plane groups for the iso norm pass: enough (group,row) items to fill the chip
@@ -1390,6 +1404,34 @@ int run_forward_gen(const admm_tv_desc& d, const Layout& Lo, const T* xin, const
         ProfScope ps(3, st);
         if (int e = grow_fwd(cb, cspec, twW, W, crows, st, gs, ld)) return e;  // r_1 = b
     }
+    if constexpr (!kF64<T>) {
+        if (Lo.odd && !train) {
+            // the two-launch iteration (odd_kernels.hpp): the column pass in place on spec[cur], then pass A
+            // (inverse rows, step, forward rows) from spec[cur] into spec[1 - cur]; u ping-pong as below
+            C* sp[2] = {cspec, at<C>(ws, Lo.spec2) + so};
+            const int rs = admm_odd::strip_rows(W);
+            const int ns = (H + rs - 1) / rs;
+            int cur = 0, ui = 0;
+            for (int it = 1; it <= d.maxit; ++it) {
+                {
+                    ProfScope ps(1, st);
+                    if (int e = gcol<T>(sp[cur], nullptr, fcT, mT, twH, H, W, np, 0, st, gs, Lo.mm, ld)) return e;
+                }
+                if (it == d.maxit) {
+                    ProfScope ps(3, st);
+                    return grow_inv<T>(sp[cur], cout, twW, W, crows, st, gs, Lo.mmr, ld);
+                }
+                ProfScope ps(0, st);
+                OddPassAArgs oa{sp[cur], sp[1 - cur], cb, u[2 * ui] + io, u[2 * ui + 1] + io, u[2 * (1 - ui)] + io,
+                                u[2 * (1 - ui) + 1] + io, lam, rho, H, ld, ns, np * ns};
+                const hipError_t he = admm_odd::pass_a(W, oa, it == 1, st);
+                if (he != hipSuccess) return fail(ADMM_TV_EHIP, std::string("k_pass_a_odd: ") + hipGetErrorString(he));
+                cur = 1 - cur;
+                ui = 1 - ui;
+            }
+            return 0;
+        }
+    }
     int uin = 0;
     for (int it = 1; it <= d.maxit; ++it) {
         const bool last = it == d.maxit;
@@ -2066,10 +2108,20 @@ extern "C" {
 int admm_tv_abi_version(void) { return ADMM_TV_ABI_VERSION; }
 
 int admm_tv_supported(int64_t H, int64_t W) {
-    return supported_hw(H, W) ? 1 : mixed_hw(H, W) ? 3 : generic_hw(H, W) ? 2 : 0;
+    return supported_hw(H, W) ? 1 : mixed_hw(H, W) ? 3 : odd_hw(H, W) ? 4 : generic_hw(H, W) ? 2 : 0;
 }
 
 int admm_tv_supported_f64(int64_t H, int64_t W) { return f64_hw(H, W) ? 1 : 0; }
+
+int admm_tv_path(const admm_tv_desc* d, int train) {
+    if (int e = validate(d)) return e;
+    if (is_f64(*d)) return ADMM_TV_PATH_GENERIC;  // the generic kernels' double instantiation
+    const Layout Lo = make_layout(*d);
+    if (!Lo.gen) return ADMM_TV_PATH_FUSED;
+    if (Lo.mixed && (!train || Lo.mixed_train)) return ADMM_TV_PATH_MIXED;
+    if (Lo.odd && !train) return ADMM_TV_PATH_ODD;
+    return ADMM_TV_PATH_GENERIC;
+}
 
 const char* admm_tv_last_error(void) { return g_err.c_str(); }
 

@@ -407,7 +407,7 @@ __device__ __forceinline__ C* gfft_lds(C* bufA, C* bufB, const GPlan& pl, int li
 // One wave per table entry: the M-term sum of a B entry is split over the wave's lanes (a fixed
 // lane-stride order and a fixed butterfly reduction, so the tables are deterministic); a thread
 // per entry made the setup a 100-us serial chain of 2M fp64 sincospi per B entry.
-__global__ void k_blue_tables(cf* __restrict__ tab, GPlan pl) {
+static __global__ void k_blue_tables(cf* __restrict__ tab, GPlan pl) {
     const int lane = threadIdx.x & 63;
     const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);  // wave-uniform
     for (int s = 0; s < pl.nst; ++s) {
