@@ -18,7 +18,6 @@
 #include "knobs.hpp"
 #include "mixed_capi.hpp"
 #include "odd_capi.hpp"
-#include "odd_kernels.hpp"
 #include "admm_tv.h"
 
 using namespace admm;

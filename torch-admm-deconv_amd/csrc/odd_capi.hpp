@@ -6,7 +6,21 @@
 #include "admm_kernels.hpp"
 
 namespace admm {
-struct OddPassAArgs;
+// arguments of the fused odd-length row pass (odd_kernels.hpp k_pass_a_odd)
+struct OddPassAArgs {
+    const cf* sin;    // x half spectra (output of the column pass)   [P][H][ld]
+    cf* sout;         // r half spectra for the next column pass       [P][H][ld]
+    const float* b;   // H_t(xin)                                      [P][H][W]
+    const float* uxi; // u_{k-1}
+    const float* uyi;
+    float* uxo;       // u_k
+    float* uyo;
+    const float* lam;
+    const float* rho;
+    int H, ld;        // rows per plane, spectrum row pitch (complex values, >= W/2 + 1)
+    int ns;           // strips per plane
+    long long nstrips;  // P ns
+};
 }
 
 namespace admm_odd {

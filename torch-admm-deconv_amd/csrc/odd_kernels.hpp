@@ -31,6 +31,7 @@
 // of the transforms; every rounding is explicit (-ffp-contract=off).
 #pragma once
 #include "generic_kernels.hpp"
+#include "odd_capi.hpp"
 
 namespace admm {
 
@@ -132,20 +133,6 @@ template <int W1, int W2> __device__ __forceinline__ int odd_npos(int n) {
     return ((n * A) % W1) * W2 + (n * B) % W2;
 }
 
-struct OddPassAArgs {
-    const cf* sin;    // x half spectra (output of the column pass)   [P][H][ld]
-    cf* sout;         // r half spectra for the next column pass       [P][H][ld]
-    const float* b;   // H_t(xin)                                      [P][H][W]
-    const float* uxi; // u_{k-1}
-    const float* uyi;
-    float* uxo;       // u_k
-    float* uyo;
-    const float* lam;
-    const float* rho;
-    int H, ld;        // rows per plane, spectrum row pitch (complex values, >= W/2 + 1)
-    int ns;           // strips per plane
-    long long nstrips;  // P ns
-};
 
 // LDS bytes of one wave: NLD + 1 lines of W complex values, then the w_x row (W floats)
 template <int W, int NLD> __host__ __device__ constexpr int odd_wave_lds() {
@@ -217,6 +204,37 @@ __global__ void __launch_bounds__(256) k_pass_a_odd(OddPassAArgs a) {
             }
         });
     }
+    // The step's u / b rows are loaded one row ahead of their use (row 0's are in flight during the
+    // inverse transforms), and a row's u stores are issued one row later, after the next prefetch: the
+    // strip walk is sequential, and gfx9's vmcnt counts stores too, so waiting for a prefetch would
+    // otherwise also wait for the stores just issued.  Every load is unconditional (lanes past the row
+    // end read its last pixel), so each iteration issues the same operations and the waits stay exact.
+    // The row streams go through buffer resources of one row each (W floats): a lane past the row end has
+    // an out-of-range offset, so its load returns 0 and its store is dropped by the hardware -- no per-lane
+    // branch around a memory instruction (an exec-skip branch there made the compiler's waits conservative).
+    constexpr int kNT = 2;  // cache policy of the streams: non-temporal (as the fused pass A, ADMM_NT)
+    auto rowbuf = [&](const float* base, int ro) {
+        return make_rsrc(base + (size_t)grow(ro) * W, (unsigned)(W * sizeof(float)));
+    };
+    // two register sets of prefetched rows, used alternately (the loop below is unrolled by two, so no
+    // register copy forces an early wait): pf[s][0..2] = u_x, u_y, b
+    float pf[2][3][JP];
+    auto load_row = [&](int ro, auto sc) {
+        constexpr int S = decltype(sc)::value;
+        const rsrc_t rx = rowbuf(a.uxi, ro), ry = rowbuf(a.uyi, ro), rb = rowbuf(a.b, ro);
+#pragma unroll
+        for (int j = 0; j < JP; ++j) {
+            const int off = (lane + 64 * j) * (int)sizeof(float);
+            pf[S][0][j] = pf[S][1][j] = 0.f;
+            if constexpr (!FIRST) {
+                pf[S][0][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, kNT));
+                pf[S][1][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, off, 0, kNT));
+            }
+            // (the row below the strip: loaded for a uniform stream, unused)
+            pf[S][2][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, kNT));
+        }
+    };
+    load_row(0, std::integral_constant<int, 0>{});
     xsync<0>();
     // 2. inverse DFTs of lines 0 .. nlf: W1-point along the first axis, W2-point along the second
     odd_stage<+1, W1, W2, 1, W2, LS, NL>(X, 0, nlf + 1, lane);
@@ -240,24 +258,25 @@ __global__ void __launch_bounds__(256) k_pass_a_odd(OddPassAArgs a) {
         const int c = ro < 0 ? 0 : (ro >= nr ? 1 : (ro & 1));
         return reinterpret_cast<float*>(X + l * LS) + c;
     };
-    float wxp[JP], wyp[JP], bp[JP];
-#pragma unroll 1
-    for (int ro = 0; ro <= nr; ++ro) {
-        const size_t go = (size_t)grow(ro) * W;
-        const bool own = ro < nr;  // ro == nr: the row below the strip (its w only)
-        float ux[JP], uy[JP], bb[JP];
+    float wxp[JP], wyp[JP], bp[JP], sux[JP], suy[JP];
+    auto store_u = [&](int ro) {  // u of strip row ro (computed one iteration earlier)
+        const rsrc_t rx = rowbuf(a.uxo, ro), ry = rowbuf(a.uyo, ro);
 #pragma unroll
         for (int j = 0; j < JP; ++j) {
-            const int n = lane + 64 * j;
-            ux[j] = uy[j] = bb[j] = 0.f;
-            if (n < W) {
-                if constexpr (!FIRST) {
-                    ux[j] = __builtin_nontemporal_load(a.uxi + go + n);
-                    uy[j] = __builtin_nontemporal_load(a.uyi + go + n);
-                }
-                if (own) bb[j] = __builtin_nontemporal_load(a.b + go + n);
-            }
+            const int off = (lane + 64 * j) * (int)sizeof(float);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, sux[j]), rx, off, 0, kNT);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, suy[j]), ry, off, 0, kNT);
         }
+    };
+    // one row: w (and, for the strip's own rows, u) of row ro, then r of row ro - 1
+    auto step_row = [&](int ro, auto ownc, auto sc) {
+        constexpr bool OWN = decltype(ownc)::value;  // false: the row below the strip (its w only)
+        constexpr int S = decltype(sc)::value;       // the register set holding this row's u / b
+        const float(&ux)[JP] = pf[S][0];
+        const float(&uy)[JP] = pf[S][1];
+        const float(&bb)[JP] = pf[S][2];
+        if constexpr (OWN) load_row(ro + 1, std::integral_constant<int, 1 - S>{});  // in flight meanwhile
+        if (ro > 0) store_u(ro - 1);
         const float* xc = xrow(ro);
         const float* xu = xrow(ro - 1);
         float wx[JP], wy[JP];
@@ -272,10 +291,8 @@ __global__ void __launch_bounds__(256) k_pass_a_odd(OddPassAArgs a) {
                 const float nux = ax - zx, nuy = ay - zy;
                 wx[j] = zx - nux;
                 wy[j] = zy - nuy;
-                if (own) {
-                    __builtin_nontemporal_store(nux, a.uxo + go + n);
-                    __builtin_nontemporal_store(nuy, a.uyo + go + n);
-                }
+                sux[j] = nux;
+                suy[j] = nuy;
             }
         }
         if (ro > 0) {  // r of the row above: b + rho ((w_x - w_x right) + (w_y - w_y below))
@@ -290,17 +307,28 @@ __global__ void __launch_bounds__(256) k_pass_a_odd(OddPassAArgs a) {
                 }
             }
         }
-        xsync<0>();  // every lane has read the previous row's w_x
+        if constexpr (OWN) {
+            xsync<0>();  // every lane has read the previous row's w_x
 #pragma unroll
-        for (int j = 0; j < JP; ++j) {
-            const int n = lane + 64 * j;
-            if (n < W) wxb[n] = wx[j];
-            wxp[j] = wx[j];
-            wyp[j] = wy[j];
-            bp[j] = bb[j];
+            for (int j = 0; j < JP; ++j) {
+                const int n = lane + 64 * j;
+                if (n < W) wxb[n] = wx[j];
+                wxp[j] = wx[j];
+                wyp[j] = wy[j];
+                bp[j] = bb[j];
+            }
+            xsync<0>();
         }
-        xsync<0>();
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+#pragma unroll 1
+    for (int ro = 0; ro < nr; ro += 2) {
+        step_row(ro, std::true_type{}, I0{});
+        if (ro + 1 < nr) step_row(ro + 1, std::true_type{}, I1{});
     }
+    if (nr & 1) step_row(nr, std::false_type{}, I1{});
+    else step_row(nr, std::false_type{}, I0{});
     if (nr & 1) {  // the last data line's second row does not exist: zero it before the forward DFT
         float* xz = xrow(nr - 1) + 1;
 #pragma unroll
