@@ -9,7 +9,7 @@ using namespace admm;
 
 namespace {
 
-constexpr int kThreads = 256;  // 4 independent waves per block (a launch granule, no barrier)
+constexpr int kThreads = ADMM_ODD_NT;  // independent waves per block x 64 (a launch granule, no barrier)
 
 template <int W1, int W2, int NLD> struct Inst {
     static constexpr int W = W1 * W2;
@@ -28,8 +28,12 @@ template <int W1, int W2, int NLD> struct Inst {
     }
 };
 
-// instances: BSD's 481 = 13 * 37 (3 row pairs + the halo line per wave: 17.3 KB of LDS)
-using I481 = Inst<13, 37, 3>;
+// instances: BSD's 481 = 13 * 37 (3 row pairs + the halo line per wave: 17.3 KB of LDS; A/B builds:
+// -DADMM_ODD_NLD row pairs per wave)
+#ifndef ADMM_ODD_NLD
+#define ADMM_ODD_NLD 3
+#endif
+using I481 = Inst<13, 37, ADMM_ODD_NLD>;
 
 }  // namespace
 

@@ -139,8 +139,21 @@ template <int W, int NLD> __host__ __device__ constexpr int odd_wave_lds() {
     return (NLD + 1) * W * 8 + ((W * 4 + 15) / 16) * 16;
 }
 
+// threads per block (whole waves, each on its own strip; A/B builds: -DADMM_ODD_NT) and an optional
+// occupancy target in waves per SIMD (-DADMM_ODD_MINW; 0: the compiler's choice).  Two-wave blocks
+// (34.6 KB of LDS) measured best at BSD size, interleaved on one box (profiles/r06_ab_odd_launch.txt):
+// 5,703-5,719 it/s against 5,487-5,530 with four-wave blocks (a CU then holds 2 of them, 8 waves, and
+// no column-pass block beside them), 5,563-5,625 with one-wave blocks, 5,504-5,542 with three; strips of
+// 4 rows (NLD 2, 13.5 KB per wave) 5,466-5,582; a 168-VGPR cap (3 waves per SIMD, 16 B spill) 5,658-5,669.
+#ifndef ADMM_ODD_NT
+#define ADMM_ODD_NT 128
+#endif
+#ifndef ADMM_ODD_MINW
+#define ADMM_ODD_MINW 0
+#endif
 template <int W1, int W2, int NLD, bool FIRST>
-__global__ void __launch_bounds__(256) k_pass_a_odd(OddPassAArgs a) {
+__global__ void __launch_bounds__(ADMM_ODD_NT) __attribute__((amdgpu_waves_per_eu(ADMM_ODD_MINW > 0 ? ADMM_ODD_MINW : 1)))
+k_pass_a_odd(OddPassAArgs a) {
     constexpr int W = W1 * W2, Wh = (W + 1) / 2, NL = NLD + 1, LS = W, RS = 2 * NLD;
     constexpr int JP = (W + 63) / 64;   // pixel slots of a lane (pixel n = lane + 64 j)
     constexpr int JK = (Wh + 63) / 64;  // half-spectrum slots of a lane (bin k = lane + 64 j)
