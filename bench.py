@@ -103,6 +103,9 @@ def parse():
     ap.add_argument("--no-extras", action="store_true",
                     help="c3: skip the extra measurements after the timed region (C3 at 100 iterations, C3 iso, "
                          "the generic-size bsd / hd workloads, the training step)")
+    ap.add_argument("--no-c5-extra", action="store_true",
+                    help="c3: skip the whole C5 model step after the other extras (its first step compiles MIOpen's "
+                         "kernels: minutes on a fresh box)")
     ap.add_argument("--cpu-planes", type=int, default=6, help="CPU baseline sample: planes of 1024^2")
     ap.add_argument("--cpu-iters", type=int, default=36, help="CPU baseline sample: timed iterations")
     ap.add_argument("--batch", type=int, default=None,
@@ -368,31 +371,22 @@ def cpu_baseline_c5(H=128, B=1, steps=2):
                       f"{B * H * H}/{Bc * Hc * Wc}"}
 
 
-def run_c5(args, world, rank, dev):
-    """Config 5 (SURVEY §8 row f1): one training step of the reference's training model
-    (scripts/train.py:70-73: two learnable iso ADMM-TV modules, 100 iterations each, then the
-    attention CNN), autograd through the HIP solver.  The reference trains with an SSIM-Lab loss
-    from its metrics package (out of scope); the step here uses L1 -- the loss is a few
-    elementwise ops next to the model.  N > 1: DDP over RCCL (gradient all-reduce, a real exchange
-    step), weak scaling (batch 16 per GPU)."""
-    from admmtor import _native
+def c5_session(dev, B, rank=0, world=1, ckpt=True, channels_last=False, conv_benchmark=False):
+    """The config-5 training step (scripts/train.py:70-73): DivergentRestorer with two learnable iso ADMM-TV
+    modules of 100 iterations, bf16 autocast, L1 loss, AdamW; autograd through the HIP solver.  Returns
+    step() -> loss.  ckpt: the 8- and 32-branch levels recompute their branches in the backward (exact;
+    without it the activations of batch 16 at 512^2 exceed 288 GB -- measured: OOM at 282 GiB allocated)."""
     from admmtor.modelbuild.blocks import set_branch_checkpointing
     from admmtor.modelbuild.denoiser import DivergentRestorer
     from admmtor.synth import CONFIG_SEED, clean_images
-    B, C, H, W, _, _, maxit, _, desc = CONFIGS["c5"]
-    reduced = (args.c5_batch or args.batch) is not None and (args.c5_batch or args.batch) != B
-    B = args.c5_batch or args.batch or B
-    if reduced:  # launch rehearsals only; the line names the reduced workload
-        desc += f" [REDUCED: batch {B} per GPU]"
+    _, C, H, W, _, _, maxit, _, _ = CONFIGS["c5"]
     deconv = {"kern_size": (), "max_iters": maxit, "iso": True}
     torch.manual_seed(CONFIG_SEED + 5)
     model = DivergentRestorer([2, 8, 32], 3, 3, 86, 86, 8, output_activation=torch.nn.Sigmoid(),
                               admms=[dict(deconv), dict(deconv)]).to(dev)
-    # the 8- and 32-branch levels recompute their branches in the backward (exact; without it the
-    # activations of batch 16 at 512^2 exceed 288 GB -- measured: OOM at 282 GiB allocated)
-    if not args.c5_no_ckpt:
+    if ckpt:
         set_branch_checkpointing(model, True)
-    if args.c5_channels_last:
+    if channels_last:
         model = model.to(memory_format=torch.channels_last)
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
@@ -401,9 +395,9 @@ def run_c5(args, world, rank, dev):
     y = clean_images(B, C, H, W, seed=CONFIG_SEED + 5 + 1000 * rank, device=dev)
     g = torch.Generator(device=dev).manual_seed(CONFIG_SEED + 5 + rank)
     x = (y + 0.06 * torch.randn(y.shape, generator=g, device=dev)).clamp_(0, 1)
-    if args.c5_conv_benchmark:
+    if conv_benchmark:
         torch.backends.cudnn.benchmark = True
-    if args.c5_channels_last:
+    if channels_last:
         x = x.contiguous(memory_format=torch.channels_last)
         y = y.contiguous(memory_format=torch.channels_last)
 
@@ -415,16 +409,69 @@ def run_c5(args, world, rank, dev):
         loss.backward()
         opt.step()
         return loss
+    return step
 
-    if rank == 0:  # heartbeat: the first step (MIOpen kernel searches) can take minutes on a fresh box
-        import threading
-        t_start = time.time()
 
-        def beat():
-            while True:
-                time.sleep(30)
-                print(f"c5 alive {time.time() - t_start:.0f} s", file=sys.stderr, flush=True)
-        threading.Thread(target=beat, daemon=True).start()
+def heartbeat(tag):
+    """stderr progress every 30 s (the first C5 step compiles MIOpen's kernels: minutes on a fresh box)."""
+    import threading
+    t_start = time.time()
+
+    def beat():
+        while True:
+            time.sleep(30)
+            print(f"{tag} alive {time.time() - t_start:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
+def c5_extra(dev, steps=2, warmup=1):
+    """The whole config-5 model step on the default line: steps/s, the ADMM kernels'
+    share of it (the library's per-launch events) and the peak memory, at the full 16x3x512^2 shape, after
+    the other extras (their tensors freed)."""
+    from admmtor import _native
+    B, C, H, W, _, _, maxit, _, desc = CONFIGS["c5"]
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)
+    step = c5_session(dev, B)
+    heartbeat("c5 extra")
+    t0 = time.perf_counter()
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t_warm = time.perf_counter() - t0
+    _native.profile_reset()
+    _native.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    T = time.perf_counter() - t0
+    _native.profile_enable(False)
+    ms, cnt = _native.profile_read()
+    return {"c5": {"workload": desc, "value": steps / T, "unit": "steps/s", "ms_per_step": T / steps * 1e3,
+                   "steps": steps, "warmup": warmup, "warmup_s": t_warm, "dtype": "bf16 autocast (ADMM solve f32)",
+                   "admm_share": {"ms_per_step_in_admm_kernels": sum(ms) / steps,
+                                  "fraction": sum(ms) / 1e3 / T, "launches_per_step": sum(cnt) / steps},
+                   "peak_mem_GiB": torch.cuda.max_memory_allocated(dev) / 2**30,
+                   "loss_finite": bool(torch.isfinite(loss.detach()))}}
+
+
+def run_c5(args, world, rank, dev):
+    """Config 5 (SURVEY §8 row f1): one training step of the reference's training model
+    (scripts/train.py:70-73: two learnable iso ADMM-TV modules, 100 iterations each, then the
+    attention CNN), autograd through the HIP solver.  The reference trains with an SSIM-Lab loss
+    from its metrics package (out of scope); the step here uses L1 -- the loss is a few
+    elementwise ops next to the model.  N > 1: DDP over RCCL (gradient all-reduce, a real exchange
+    step), weak scaling (batch 16 per GPU)."""
+    from admmtor import _native
+    B, C, H, W, _, _, maxit, _, desc = CONFIGS["c5"]
+    reduced = (args.c5_batch or args.batch) is not None and (args.c5_batch or args.batch) != B
+    B = args.c5_batch or args.batch or B
+    if reduced:  # launch rehearsals only; the line names the reduced workload
+        desc += f" [REDUCED: batch {B} per GPU]"
+    step = c5_session(dev, B, rank, world, not args.c5_no_ckpt, args.c5_channels_last, args.c5_conv_benchmark)
+    if rank == 0:
+        heartbeat("c5")
     for i in range(args.warmup):
         step()
         torch.cuda.synchronize()
@@ -513,6 +560,21 @@ def launch_ranks(n, argv):
     return subprocess.run(launch_cmd(n, argv, port), env=env).returncode
 
 
+def rocfft_rank_cache(local_rank):
+    """Give this rank its own rocFFT kernel cache before anything touches the GPU.
+
+    rocFFT keeps the kernels it compiles at run time in a per-user sqlite database (WAL journal) that every
+    process of the user opens.  In the round-5 rehearsal the ranks stalled at their first device FFT when the
+    parent process (a pytest run) had used rocFFT before launching them: a process that keeps the database
+    open holds its read snapshot, and a writer's WAL checkpoint then waits for it.  Each rank now uses a
+    cache file of its own (ROCFFT_RTC_CACHE_PATH, unless the caller set one); the shipped read-only system
+    cache is unaffected."""
+    if "ROCFFT_RTC_CACHE_PATH" not in os.environ:
+        import tempfile
+        os.environ["ROCFFT_RTC_CACHE_PATH"] = os.path.join(
+            tempfile.gettempdir(), f"admmtor_rocfft_uid{os.getuid()}_rank{local_rank}.db")
+
+
 def main():
     args = parse()
     world, launch = resolve_world(args.gpus, os.environ)
@@ -521,6 +583,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        rocfft_rank_cache(local)
         # rehearsal on a 1-GPU box (never set by the driver): every rank on cuda:0 over gloo
         if os.environ.get("ADMM_BENCH_REHEARSAL"):
             local = 0
@@ -550,13 +613,10 @@ def main():
             print(f"bench rank 0/{world}: {msg}", file=sys.stderr, flush=True)
 
     progress("process group up")
-    # rank-local shard of synthetic blurred images, generated directly in HBM
+    # rank-local shard of synthetic blurred images, generated directly in HBM (torch.fft on the device; each
+    # rank has its own rocFFT kernel cache, rocfft_rank_cache)
     psf = make_psf(kind, k).to(dev) if k else torch.empty(0, device=dev)
-    # N > 1: each rank synthesises its shard on the host and copies it in, so the ranks never touch
-    # rocFFT (torch.fft on the device): rehearsed on one GPU under a parent process that had used it,
-    # the ranks' first device FFT stalled (rocFFT's kernel cache); the solve itself does not use rocFFT
-    x = blurred_batch(B, C, H, W, psf.cpu(), seed=CONFIG_SEED + 2 + 1000 * rank,
-                      device="cpu" if world > 1 else dev).to(dev)
+    x = blurred_batch(B, C, H, W, psf.cpu(), seed=CONFIG_SEED + 2 + 1000 * rank, device=dev)
     lam = torch.tensor([0.01], device=dev)
     rho = torch.tensor([0.02], device=dev)
     torch.cuda.synchronize()
@@ -678,6 +738,8 @@ def main():
         torch.cuda.empty_cache()
         extras.update(generic_extras(dev, args.no_parity))
         extras.update(train_extra(dev))
+        if not args.no_c5_extra:
+            extras.update(c5_extra(dev))
     result = None
     if rank == 0:
         cpu = None

@@ -102,3 +102,14 @@ def test_workload_labels_agree_with_the_path():
     assert bench.path_of(1024, 1024) == "fused" and bench.path_of(1080, 1920) == "fused mixed-radix"
     assert bench.path_of(15, 17) == "generic" and bench.path_of(321, 481) == "fused odd-length"
     assert bench.path_of(321, 481, iso=True) == "generic"  # iso keeps the generic kernels there
+
+
+def test_rocfft_rank_cache(monkeypatch):
+    """Each rank gets its own rocFFT kernel-cache file unless the caller chose one."""
+    monkeypatch.delenv("ROCFFT_RTC_CACHE_PATH", raising=False)
+    bench.rocfft_rank_cache(3)
+    path = os.environ["ROCFFT_RTC_CACHE_PATH"]
+    assert path.endswith("_rank3.db") and f"uid{os.getuid()}" in path
+    monkeypatch.setenv("ROCFFT_RTC_CACHE_PATH", "/somewhere/mine.db")
+    bench.rocfft_rank_cache(5)
+    assert os.environ["ROCFFT_RTC_CACHE_PATH"] == "/somewhere/mine.db"

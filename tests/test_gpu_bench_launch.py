@@ -12,12 +12,12 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run_bench(n, tmo=280):
+def _run_bench(n, tmo=280, config="c3"):
     env = dict(os.environ, ADMM_BENCH_REHEARSAL="1")
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "ROCFFT_RTC_CACHE_PATH"):
         env.pop(k, None)
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--batch", "1", "--steps", "1",
-           "--warmup", "0", "--no-cpu-baseline", "--no-parity", "--no-extras"]
+           "--warmup", "0", "--no-cpu-baseline", "--no-parity", "--no-extras", "--config", config]
     # stderr (torchrun's and the ranks' progress lines) streams through, so a slow start stays visible
     p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True, timeout=tmo, cwd=ROOT)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -36,3 +36,23 @@ def test_bench_gpus_n_launches_n_ranks(cuda_dev, n):
     assert res["config"]["reduced_batch"] is True and res["config"]["batch_per_gpu"] == 1
     assert res["config"]["parallelism"].startswith(f"shard{n} ")
     assert res["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 8])
+def test_ranks_synthesise_on_device_after_parent_used_rocfft(cuda_dev, n):
+    """the ranks' first device FFT stalled when the parent process had used rocFFT
+    (its per-user kernel-cache database, held open by the parent).  This parent runs device FFTs of the BSD
+    sizes (run-time compiled Bluestein kernels, written to its cache) and keeps rocFFT loaded; then N
+    rehearsal ranks synthesise their BSD shards with torch.fft on the device, each with its own cache
+    (bench.rocfft_rank_cache), and the run completes."""
+    import torch
+    x = torch.rand(2, 3, 321, 481, device=cuda_dev)
+    y = torch.fft.irfftn(torch.fft.rfftn(x, dim=(2, 3)), s=(321, 481), dim=(2, 3))
+    torch.cuda.synchronize()
+    assert torch.allclose(x, y, atol=1e-5)
+    p, lines = _run_bench(n, config="bsd")
+    assert p.returncode == 0, p.stdout[-3000:]
+    res = json.loads(lines[-1])
+    print(f"bsd --gpus {n} after a parent rocFFT: n_gpus={res['n_gpus']} value={res['value']:.1f}")
+    assert res["n_gpus"] == n and res["config"]["path"] == "fused odd-length"
