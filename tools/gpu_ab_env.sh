@@ -15,7 +15,7 @@ mkdir -p gpurun_out
 for round in 1 2; do
   for setting in "$@"; do
     echo "round $round: $setting" >> "$OUT"
-    env $setting timeout -k 10 240 python3 bench.py --config "$CFG" --steps 10 --warmup 2 --no-cpu-baseline \
+    env $setting timeout -k 10 240 python3 bench.py --config "$CFG" --steps 10 --warmup 2 --no-cpu-baseline --no-extras \
       --no-parity >> "$OUT" 2>/dev/null || { echo "bench failed: $setting"; exit 1; }
   done
 done
