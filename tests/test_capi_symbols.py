@@ -52,7 +52,8 @@ def test_host_entry_points():
     assert lib.admm_tv_abi_version() == 7
     fast, generic = 1, 2
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (16, 2048), (4096, 16))] == [fast] * 3
-    assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 8192), (8, 64), (1, 1), (481, 321))] == [generic] * 5
+    assert [lib.admm_tv_supported(*hw) for hw in ((15, 17), (1024, 8192), (8, 64), (1, 1), (509, 321))] == [generic] * 5
+    assert [lib.admm_tv_supported(*hw) for hw in ((321, 481), (481, 321))] == [4] * 2  # odd-length rows, either way
     assert [lib.admm_tv_supported(*hw) for hw in ((4097, 16), (5000, 33))] == [generic] * 2  # beyond 4096
     assert [lib.admm_tv_supported(*hw) for hw in ((65537, 16), (16, 70000), (0, 16))] == [0] * 3
     # smooth sizes with transform plans: the fused iteration on mixed-radix transforms (inference)

@@ -39,7 +39,7 @@ def test_supported_codes():
                                                   (600, 800), (768, 1024), (1200, 1600), (1536, 2048), (1080, 1440),
                                                   (1440, 2560), (800, 800))] == [3] * 17
     assert [lib.admm_tv_supported(*hw) for hw in ((1024, 1024), (4096, 2048))] == [1] * 2
-    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1921), (1080, 7680), (1000, 1920), (481, 321))] == [2] * 4
+    assert [lib.admm_tv_supported(*hw) for hw in ((1080, 1921), (1080, 7680), (1000, 1920), (509, 509))] == [2] * 4
 
 
 CASES = [

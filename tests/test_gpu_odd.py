@@ -36,7 +36,10 @@ def test_odd_path_codes():
     from admmtor import _native
     lib = _native.load()
     assert [lib.admm_tv_supported(*hw) for hw in ((321, 481), (1, 481), (4096, 481), (17, 481))] == [4] * 4
-    assert [lib.admm_tv_supported(*hw) for hw in ((481, 321), (509, 509), (1080, 1921))] == [2] * 3
+    assert [lib.admm_tv_supported(*hw) for hw in ((481, 321), (481, 1), (481, 17))] == [4] * 3  # transposed
+    assert [lib.admm_tv_supported(*hw) for hw in ((509, 509), (1080, 1921), (481, 481))] == [2] * 3
+    assert _native.path(_native.desc(1, 3, 481, 321, 9, False, 10)) == "fused odd-length"
+    assert _native.path(_native.desc(1, 3, 481, 321, 9, False, 10), train=True) == "generic"
     d = _native.desc(2, 3, 321, 481, 9, False, 10)
     assert _native.path(d) == "fused odd-length" and _native.path(d, train=True) == "generic"
     assert _native.path(_native.desc(2, 3, 321, 481, 9, True, 10)) == "generic"  # iso: the generic kernels
@@ -134,3 +137,27 @@ def test_odd_size_iso_and_training_keep_generic(cuda_dev):
     want = torch.autograd.grad(ref, (xr, lr), cot.double())
     assert rel(out.detach().cpu(), ref.detach()) <= TOL_REF64
     assert rel(got[0].cpu(), want[0]) <= 1e-3 and rel(got[1].cpu(), want[1]) <= 1e-3
+
+
+@pytest.mark.parametrize("shape,psf,it", [((2, 3, 481, 321), ("gauss:1.5", 9), 20), ((1, 2, 481, 17), ("motion", 5), 10),
+                                          ((1, 1, 481, 1), None, 6)])
+def test_odd_transposed_orientation(cuda_dev, monkeypatch, shape, psf, it):
+    """A portrait odd-width image (H = 481, the BSD portrait frames) runs as its transpose on the odd-length
+    iteration (Layout::tr): the solve commutes with transposing the image and the PSF (Dx and Dy trade
+    places), so the result is the landscape solve of the transposed input, transposed back -- bit for bit --
+    and within the gate of the fp64 oracle and of the generic kernels."""
+    from admmtor import _native
+    from admmtor.synth import blurred_batch, make_psf
+    k = make_psf(*psf) if psf else None
+    x = blurred_batch(*shape, k if k is not None else torch.empty(0), seed=sum(shape) + it)
+    got = solve(x, k, False, it, cuda_dev)
+    kt = k.transpose(-1, -2).contiguous() if k is not None else None
+    land = solve(x.transpose(-1, -2).contiguous(), kt, False, it, cuda_dev)
+    assert torch.equal(got, land.transpose(-1, -2))
+    ref = oracle(x, k, False, it)
+    monkeypatch.setenv("ADMM_ODD", "0")
+    with _native.ab_library():
+        gen = solve(x, k, False, it, cuda_dev)
+    e_ref, e_gen, e_gen_ref = rel(got, ref), rel(got, gen), rel(gen, ref)
+    print(shape, psf, it, f"transposed odd vs fp64 oracle {e_ref:.2e}, vs generic {e_gen:.2e} (generic {e_gen_ref:.2e})")
+    assert e_ref <= TOL_REF64 and e_gen <= 2 * max(e_gen_ref, 1e-7) + e_ref

@@ -123,6 +123,14 @@ bool mixed_hw(int64_t H, int64_t W) {
 bool odd_hw(int64_t H, int64_t W) {
     return generic_hw(H, W) && !mixed_hw(H, W) && admm_odd::row_ok((int)W) && env_int("ADMM_ODD", 1) != 0;
 }
+// ... and the transposed orientation (H an odd-path row length, W not: BSD portrait frames, 481 x 321): the
+// solve commutes with transposing the image and the PSF (Dx and Dy trade places; the x-update's
+// |Dx^|^2 + |Dy^|^2, the shrinkage and the centred H_t are symmetric in them), so the aniso inference solve
+// transposes xin and the PSF, runs the odd-length iteration on the W x H problem and transposes the result
+// back (two transposes per solve, not per iteration; Layout::tr)
+bool odd_t_hw(int64_t H, int64_t W) {
+    return generic_hw(H, W) && !mixed_hw(H, W) && !odd_hw(H, W) && odd_hw(W, H);
+}
 // fp64 solves (ADMM_TV_FLAG_F64) run on the generic kernels' double instantiation at every size
 bool is_f64(const admm_tv_desc& d) { return (d.flags & ADMM_TV_FLAG_F64) != 0; }
 bool f64_hw(int64_t H, int64_t W) {
@@ -161,6 +169,10 @@ struct Layout {
     // fused odd-length row pass (odd_hw, aniso inference): the second half-spectrum buffer of its ping-pong
     bool odd;
     size_t spec2;
+    // transposed odd-length solve (odd_t_hw, aniso inference): xin and the result transposed, the PSF
+    // transposed, then the W x H problem's own workspace at tws
+    bool tr;
+    size_t xT, oT, kT, tws;
     size_t rimg;  // generic path: spec[0] = half spectra [P][H][W/2+1], spec[1] = x image, rimg = r image
     size_t gscr;  // generic path, lines beyond the LDS image: the transform blocks' scratch slots
     int ngroups, ppg;
@@ -170,6 +182,13 @@ struct Layout {
     // lines (A/B knob ADMM_GEN_PITCH=0: Wh)
     int ldw;
 };
+
+admm_tv_desc transposed(const admm_tv_desc& d) {
+    admm_tv_desc t = d;
+    t.H = d.W;
+    t.W = d.H;
+    return t;
+}
 
 Layout make_layout(const admm_tv_desc& d) {
     Layout L{};
@@ -241,6 +260,22 @@ Layout make_layout(const admm_tv_desc& d) {
         L.nsq = take(G * 2 * H * W * rs);  // per module
     }
     L.total = o;
+    if (!f64 && G == 1 && !d.iso && odd_t_hw(d.H, d.W)) {
+        // the transposed inference solve: [xin^T][result^T][PSF^T][the W x H problem's workspace], laid over
+        // the regions above (a call uses one or the other: training and the helpers keep this layout)
+        size_t t = 0;
+        auto takeT = [&](size_t bytes) {
+            size_t at = t;
+            t += up(bytes);
+            return at;
+        };
+        L.tr = true;
+        L.xT = takeT(img);
+        L.oT = takeT(img);
+        L.kT = takeT((size_t)std::max(1, d.kh * d.kw) * sizeof(float));
+        L.tws = takeT(make_layout(transposed(d)).total);
+        L.total = std::max(L.total, t);
+    }
     return L;
 }
 
@@ -1665,6 +1700,24 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
     const Layout Lo = make_layout(d);
     if (!ws || ws_bytes < Lo.total || (reinterpret_cast<uintptr_t>(ws) % kAlign) != 0)
         return fail(ADMM_TV_EWORKSPACE, "workspace too small or not 256-byte aligned");
+    if (Lo.tr && !hist && d.maxit > 0) {  // the transposed odd-length solve (odd_t_hw)
+        const long long P = d.B * d.C;
+        const int H = (int)d.H, W = (int)d.W;
+        float* xT = at<float>(ws, Lo.xT);
+        float* oT = at<float>(ws, Lo.oT);
+        float* kT = d.kh > 0 ? at<float>(ws, Lo.kT) : nullptr;
+        {
+            ProfScope ps(3, s);
+            hipError_t e = admm_odd::transpose(xin, xT, H, W, P, s);
+            if (e == hipSuccess && kT) e = admm_odd::transpose(kern, kT, d.kh, d.kw, 1, s);
+            if (e != hipSuccess) return fail(ADMM_TV_EHIP, std::string("k_transpose: ") + hipGetErrorString(e));
+        }
+        const admm_tv_desc dT = transposed(d);
+        if (int e = run_forward(dT, xT, kT, lam, rho, oT, at<char>(ws, Lo.tws), ws_bytes - Lo.tws, nullptr, s)) return e;
+        ProfScope ps(3, s);
+        const hipError_t e = admm_odd::transpose(oT, out, W, H, P, s);
+        return e == hipSuccess ? 0 : fail(ADMM_TV_EHIP, std::string("k_transpose: ") + hipGetErrorString(e));
+    }
     const int G = ngroups_of(d);
     const long long Pm = d.B * d.C, P = G * Pm;  // planes of one module, of all modules
     const int H = (int)d.H, W = (int)d.W, N = W / 2;
@@ -2107,7 +2160,7 @@ extern "C" {
 int admm_tv_abi_version(void) { return ADMM_TV_ABI_VERSION; }
 
 int admm_tv_supported(int64_t H, int64_t W) {
-    return supported_hw(H, W) ? 1 : mixed_hw(H, W) ? 3 : odd_hw(H, W) ? 4 : generic_hw(H, W) ? 2 : 0;
+    return supported_hw(H, W) ? 1 : mixed_hw(H, W) ? 3 : (odd_hw(H, W) || odd_t_hw(H, W)) ? 4 : generic_hw(H, W) ? 2 : 0;
 }
 
 int admm_tv_supported_f64(int64_t H, int64_t W) { return f64_hw(H, W) ? 1 : 0; }
@@ -2116,6 +2169,7 @@ int admm_tv_path(const admm_tv_desc* d, int train) {
     if (int e = validate(d)) return e;
     if (is_f64(*d)) return ADMM_TV_PATH_GENERIC;  // the generic kernels' double instantiation
     const Layout Lo = make_layout(*d);
+    if (Lo.tr) return train ? ADMM_TV_PATH_GENERIC : ADMM_TV_PATH_ODD;
     if (!Lo.gen) return ADMM_TV_PATH_FUSED;
     if (Lo.mixed && (!train || Lo.mixed_train)) return ADMM_TV_PATH_MIXED;
     if (Lo.odd && !train) return ADMM_TV_PATH_ODD;

@@ -200,12 +200,18 @@ template <> struct MRowT<1280> {
     using Fwd = Sched<5, 8, 4, 8>;
 };
 
+#ifndef ADMM_MROW_WIDE_NT
+#define ADMM_MROW_WIDE_NT 256
+#endif
 template <int N, class PL = MRow<N>> struct MRowG {
     using P = PL;
     static constexpr int Lg = P::Lg, Lp = P::Lp, Ep = P::Ep, Ls = P::Ls, Es = P::Es, W = 2 * N;
     static constexpr int a = sched_regs<N, Lg>(typename P::Inv{}), b = sched_regs<N, Lg>(typename P::Fwd{});
     static constexpr int EM = a > b ? a : b;
-    static constexpr int NT = 256, SG = NT / Lg;
+    // threads per block: 256; wide groups A/B: -DADMM_MROW_WIDE_NT=128 (one 2-wave group per block, so a
+    // group's block barriers wait only for its own waves)
+    static constexpr int NT = (Lg > 64 && ADMM_MROW_WIDE_NT < 256 && Lg <= ADMM_MROW_WIDE_NT) ? ADMM_MROW_WIDE_NT : 256;
+    static constexpr int SG = NT / Lg;
     static constexpr bool WIDE = Lg > 64;  // the row group spans several waves: LDS exchanges, block barriers
     // wide groups synchronise their LDS exchanges with LDS-only block barriers (fft_core xsync<2>): a
     // __syncthreads would also drain the wave's outstanding global loads and stores at every exchange

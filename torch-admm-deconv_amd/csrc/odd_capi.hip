@@ -1,6 +1,8 @@
 // odd_capi.hip -- launchers of the fused odd-length row pass (odd_kernels.hpp).
 #include "odd_capi.hpp"
 
+#include <algorithm>
+
 #include "odd_kernels.hpp"
 
 namespace admm_odd {
@@ -35,7 +37,37 @@ template <int W1, int W2, int NLD> struct Inst {
 #endif
 using I481 = Inst<13, 37, ADMM_ODD_NLD>;
 
+// out[p][j][i] = in[p][i][j]: 32 x 32 tiles through LDS (odd word pitch: no bank conflicts), both sides
+// coalesced; planes on grid.z (strided beyond 65,535)
+__global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ in, float* __restrict__ out, int H, int W,
+                                                   long long P) {
+    __shared__ float t[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8 threads
+    const int j0 = blockIdx.x * 32, i0 = blockIdx.y * 32;
+    for (long long p = blockIdx.z; p < P; p += gridDim.z) {
+        const float* src = in + (size_t)p * H * W;
+        float* dst = out + (size_t)p * H * W;
+        for (int r = ty; r < 32; r += 8) {
+            const int i = i0 + r, j = j0 + tx;
+            if (i < H && j < W) t[r][tx] = src[(size_t)i * W + j];
+        }
+        __syncthreads();
+        for (int r = ty; r < 32; r += 8) {
+            const int j = j0 + r, i = i0 + tx;
+            if (i < H && j < W) dst[(size_t)j * H + i] = t[tx][r];
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
+
+hipError_t transpose(const float* in, float* out, int H, int W, long long P, hipStream_t s) {
+    if (P <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((W + 31) / 32), (unsigned)((H + 31) / 32), (unsigned)std::min<long long>(P, 65535));
+    hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, s, in, out, H, W, P);
+    return hipGetLastError();
+}
 
 bool row_ok(int W) { return W == I481::W; }
 

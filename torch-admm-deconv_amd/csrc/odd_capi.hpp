@@ -31,5 +31,7 @@ bool row_ok(int W);
 int strip_rows(int W);
 // pass A of one iteration over a.nstrips strips; first: u_{k-1} = 0 (not read)
 hipError_t pass_a(int W, const admm::OddPassAArgs& a, bool first, hipStream_t s);
+// out[p][j][i] = in[p][i][j] for P planes of H x W floats (the transposed odd-length solve, odd_t_hw)
+hipError_t transpose(const float* in, float* out, int H, int W, long long P, hipStream_t s);
 
 }  // namespace admm_odd
