@@ -37,7 +37,8 @@ def test_odd_path_codes():
     lib = _native.load()
     assert [lib.admm_tv_supported(*hw) for hw in ((321, 481), (1, 481), (4096, 481), (17, 481))] == [4] * 4
     assert [lib.admm_tv_supported(*hw) for hw in ((481, 321), (481, 1), (481, 17))] == [4] * 3  # transposed
-    assert [lib.admm_tv_supported(*hw) for hw in ((509, 509), (1080, 1921), (481, 481))] == [2] * 3
+    assert [lib.admm_tv_supported(*hw) for hw in ((509, 509), (1080, 1921), (321, 321))] == [2] * 3
+    assert lib.admm_tv_supported(481, 481) == 4  # 481-point rows (the landscape path itself)
     assert _native.path(_native.desc(1, 3, 481, 321, 9, False, 10)) == "fused odd-length"
     assert _native.path(_native.desc(1, 3, 481, 321, 9, False, 10), train=True) == "generic"
     d = _native.desc(2, 3, 321, 481, 9, False, 10)

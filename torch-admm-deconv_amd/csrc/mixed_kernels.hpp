@@ -175,6 +175,10 @@ template <> struct MRowT<540> {
     using Fwd = Sched<5, 6, 3, 6>;
 };
 template <> struct MRowT<640> {
+    // one 2-wave group per 128-thread block (its LDS barriers wait only for its own two waves): 720p inference
+    // 2,206-2,211 -> 2,338-2,339 it/s, pass A 0.310 -> 0.283 ms, interleaved (profiles/r06_ab_p720_wide_nt.txt);
+    // HD's 8-pair 960-point plan lost 1.5 % that way (profiles/r06_ab_hd_wide_nt.txt) and keeps 256 threads
+    static constexpr int NT = 128;
     static constexpr int Lg = 128, Lp = 128, Ep = 5, Ls = 80, Es = 8;
     using Inv = Sched<8, 2, 8, 5>;
     using Fwd = Sched<5, 8, 2, 8>;
@@ -203,14 +207,18 @@ template <> struct MRowT<1280> {
 #ifndef ADMM_MROW_WIDE_NT
 #define ADMM_MROW_WIDE_NT 256
 #endif
+// threads per block of a row plan: its NT member where it has one, else 256
+template <class PL, class = void> struct PlanNT : std::integral_constant<int, 256> {};
+template <class PL> struct PlanNT<PL, std::void_t<decltype(PL::NT)>> : std::integral_constant<int, PL::NT> {};
 template <int N, class PL = MRow<N>> struct MRowG {
     using P = PL;
     static constexpr int Lg = P::Lg, Lp = P::Lp, Ep = P::Ep, Ls = P::Ls, Es = P::Es, W = 2 * N;
     static constexpr int a = sched_regs<N, Lg>(typename P::Inv{}), b = sched_regs<N, Lg>(typename P::Fwd{});
     static constexpr int EM = a > b ? a : b;
-    // threads per block: 256; wide groups A/B: -DADMM_MROW_WIDE_NT=128 (one 2-wave group per block, so a
-    // group's block barriers wait only for its own waves)
-    static constexpr int NT = (Lg > 64 && ADMM_MROW_WIDE_NT < 256 && Lg <= ADMM_MROW_WIDE_NT) ? ADMM_MROW_WIDE_NT : 256;
+    // threads per block: the plan's (PlanNT); every 2-wave group alone, A/B: -DADMM_MROW_WIDE_NT=128 (one group
+    // per block, so a group's block barriers wait only for its own waves)
+    static constexpr int NT =
+        (Lg > 64 && ADMM_MROW_WIDE_NT < 256 && Lg <= ADMM_MROW_WIDE_NT) ? ADMM_MROW_WIDE_NT : PlanNT<PL>::value;
     static constexpr int SG = NT / Lg;
     static constexpr bool WIDE = Lg > 64;  // the row group spans several waves: LDS exchanges, block barriers
     // wide groups synchronise their LDS exchanges with LDS-only block barriers (fft_core xsync<2>): a
