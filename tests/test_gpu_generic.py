@@ -65,6 +65,8 @@ def test_g7_odd_size_vs_reference(cuda_dev):
     ((1, 1, 143, 121), ("gauss:1.5", 7), True, 15),        # 11*13 x 11^2: the radix-11 / 13 butterflies
     ((1, 2, 66, 130), ("motion", 7), False, 12),           # 2*3*11 x 2*5*13: radix 11 / 13 after other stages
     ((1, 1, 509, 37), ("motion", 9), False, 10),           # prime 509: Bluestein at M = 1024
+    ((1, 2, 509, 509), ("gauss:1.5", 9), False, 10),        # 509 x 509 (VERDICT r5 item 1's parity shapes)
+    ((1, 1, 1080, 1921), ("gauss:1.5", 9), False, 6),      # 1921 = 17 * 113 rows beside HD columns
     ((1, 2, 26, 1021), None, False, 8),                    # prime 1021 > 512: the direct prime stage
     ((1, 1, 214, 321), ("gauss:2", 7), True, 12),          # 2*107 x 3*107
     ((1, 1, 12, 6000), ("gauss:1.5", 9), False, 6),        # lines beyond 4096 (one line per block)
