@@ -6,7 +6,9 @@ Drop-in for ``/root/reference/src/admmtor/eops/deconv.py``:
   (deconv.py:35-40) and its error behaviour (deconv.py:42, 90-96),
   but runs the whole solver as hand-written HIP kernels for gfx950 through the
   C ABI of ``include/admm_tv.h`` (two fused HBM passes per iteration).  There is
-  no CPU fallback: host tensors raise.
+  no CPU fallback: host tensors are staged to the current GPU (``_stage``) and the
+  result is returned on that device; without a GPU or the HIP library the call
+  raises.
 * the small public helpers of the reference module (``torch_abs2``,
   ``hard_thresh``, ``soft_thresh``, ``block_thresh``, ``pixelnorm``,
   ``identity``, ``conv_circular``; deconv.py:7-32) keep their names and
