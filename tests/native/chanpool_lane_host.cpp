@@ -34,12 +34,13 @@ struct HostIo {
     uint32_t load(int c) const { return px[(size_t)c * stride]; }
     uint32_t raw(int c) const { return px[(size_t)c * stride]; }
     int opaque(int v) const { return v; }
+    u16x2 pack(uint32_t lo, uint32_t hi) const { return u16x2{(unsigned short)lo, (unsigned short)hi}; }
     void barrier() const {}
 };
 
 template <class T, int NP>
 static void run(const std::vector<uint16_t>& x, int C, long long npix, int depth, float* sd, int32_t* mi, int32_t* oi) {
-    std::vector<uint32_t> col((size_t)(C + 1) * 64);
+    std::vector<uint16_t> col((size_t)(C + 1) * 64);
     for (long long p = 0; p < npix; ++p) {
         HostIo io{x.data() + p, npix};
         int m, o;

@@ -511,6 +511,13 @@ template <class S> struct LaneIo {
         asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(v));
         return r;
     }
+    // an opaque pack: as plain vector code the compiler sank every pack to the sort and kept all NP
+    // images unpacked (one register each) until then
+    __device__ __forceinline__ u16x2 pack(uint32_t lo, uint32_t hi) const {
+        uint32_t r;
+        asm volatile("v_lshl_or_b32 %0, %2, 16, %1" : "=v"(r) : "v"(lo), "v"(hi));
+        return __builtin_bit_cast(u16x2, r);
+    }
     __device__ __forceinline__ void barrier() const { __builtin_amdgcn_sched_barrier(0); }
 };
 
@@ -520,7 +527,7 @@ __global__ void __launch_bounds__(64) k_chanpool_lane(const typename T::store* _
                                                       int16_t* __restrict__ idx, int C, long long HW,
                                                       long long npix, int depth_limit, int exp) {
     using S = typename T::store;
-    extern __shared__ __align__(16) uint32_t colmem[];
+    extern __shared__ __align__(16) uint16_t colmem[];
     const int lane = threadIdx.x;
     const long long gp = (long long)blockIdx.x * 64 + lane;
     if (gp >= npix) return;
@@ -600,7 +607,7 @@ template <class T, int NP>
 int launch_lane(const void* x, int64_t B, int64_t C, int64_t HW, void* out, int16_t* idx, int depth, hipStream_t s) {
     const long long npix = (long long)B * HW;
     hipLaunchKernelGGL((k_chanpool_lane<T, NP>), dim3((unsigned)((npix + 63) / 64)), dim3(64),
-                       (size_t)(C + 1) * 64 * sizeof(uint32_t), s, static_cast<const typename T::store*>(x),
+                       (size_t)(C + 1) * 64 * sizeof(uint16_t), s, static_cast<const typename T::store*>(x),
                        static_cast<typename T::store*>(out), idx, (int)C, (long long)HW, npix, depth,
                        env_int("ADMM_CHANPOOL_EXP", 0));  // A/B knob: phases skipped for timing (wrong results)
     return hipGetLastError() == hipSuccess ? 0 : ADMM_TV_EHIP;

@@ -98,14 +98,28 @@ template <int K, int NP> __device__ __forceinline__ void pk_blocks(u16x2 (&v)[NP
 }
 template <int NP> __device__ __forceinline__ void pk_bitonic(u16x2 (&v)[NP / 2]) { pk_blocks<2, NP>(v); }
 
-// std::__adjust_heap / __push_heap / heap sort on the lane's LDS column (keys value << 8 | channel,
-// compared by value): the depth-limit fallback, reached only by adversarial orders
-__device__ void adjust_heap_col(uint32_t* col, int f, int hole, int len, uint32_t v) {
+// The lane's LDS column holds one 16-bit element per channel: the value image (position = channel
+// while the column is in channel order).  For the introsort trace the mode-valued elements are
+// rewritten as channel codes -- images no value takes, so an element carries its channel through the
+// partitions and still compares as the mode value: below the image of -inf (the negative NaN bit
+// patterns, which ord16 folds onto 0xFFFE) and 0x7FFF (-0, folded onto +0).  bf16: codes 0..126 and
+// 0x7FFF for channel 127; f16: codes 0..1022.
+template <class T> struct ModeCode {
+    static constexpr uint32_t lim = T::inf == 0x7F80u ? 0x7Fu : 0x3FFu;
+    __device__ static uint32_t enc(int c) { return (uint32_t)c < lim ? (uint32_t)c : 0x7FFFu; }
+    __device__ static bool is(uint32_t e) { return e < lim || e == 0x7FFFu; }
+    __device__ static int chan(uint32_t e) { return e == 0x7FFFu ? 127 : (int)e; }
+};
+
+// std::__adjust_heap / __push_heap / heap sort on the lane's LDS column, compared by value (val:
+// element -> value image): the depth-limit fallback, reached only by adversarial orders
+template <class V>
+__device__ void adjust_heap_col(uint16_t* col, int f, int hole, int len, uint32_t v, const V& val) {
     const int top = hole;
     int sc = hole;
     while (sc < (len - 1) / 2) {
         sc = 2 * (sc + 1);
-        if ((col[(f + sc) * 64] >> 8) < (col[(f + sc - 1) * 64] >> 8)) --sc;
+        if (val(col[(f + sc) * 64]) < val(col[(f + sc - 1) * 64])) --sc;
         col[(f + hole) * 64] = col[(f + sc) * 64];
         hole = sc;
     }
@@ -115,31 +129,31 @@ __device__ void adjust_heap_col(uint32_t* col, int f, int hole, int len, uint32_
         hole = sc - 1;
     }
     int parent = (hole - 1) / 2;
-    while (hole > top && (col[(f + parent) * 64] >> 8) < (v >> 8)) {
+    while (hole > top && val(col[(f + parent) * 64]) < val(v)) {
         col[(f + hole) * 64] = col[(f + parent) * 64];
         hole = parent;
         parent = (hole - 1) / 2;
     }
-    col[(f + hole) * 64] = v;
+    col[(f + hole) * 64] = (uint16_t)v;
 }
-__device__ void heap_sort_col(uint32_t* col, int f, int l) {
+template <class V> __device__ void heap_sort_col(uint16_t* col, int f, int l, const V& val) {
     const int len = l - f;
     if (len >= 2)
         for (int parent = (len - 2) / 2;; --parent) {
-            adjust_heap_col(col, f, parent, len, col[(f + parent) * 64]);
+            adjust_heap_col(col, f, parent, len, col[(f + parent) * 64], val);
             if (parent == 0) break;
         }
     for (int last = l; last - f > 1;) {
         --last;
         const uint32_t v = col[last * 64];
         col[last * 64] = col[f * 64];
-        adjust_heap_col(col, f, 0, last - f, v);
+        adjust_heap_col(col, f, 0, last - f, v, val);
     }
 }
 
-// fn(p, key) over the lane's LDS column, positions [f, l) in order, eight reads issued before any use
-// (a plain loop waits out one LDS round trip per element)
-template <class F> __device__ __forceinline__ void for_channels(const uint32_t* col, int f, int l, F&& fn) {
+// fn(p, element) over the lane's LDS column, positions [f, l) in order, eight reads issued before any
+// use (a plain loop waits out one LDS round trip per element)
+template <class F> __device__ __forceinline__ void for_channels(const uint16_t* col, int f, int l, F&& fn) {
     int p = f;
     for (; p + 8 <= l; p += 8) {
         uint32_t e[8];
@@ -148,7 +162,7 @@ template <class F> __device__ __forceinline__ void for_channels(const uint32_t* 
 #pragma unroll
         for (int k = 0; k < 8; ++k) fn(p + k, e[k]);
     }
-    for (; p < l; ++p) fn(p, col[p * 64]);
+    for (; p < l; ++p) fn(p, (uint32_t)col[p * 64]);
 }
 
 // the lane kernel's 16-bit value image in straight arithmetic (ternaries here became divergent
@@ -164,58 +178,62 @@ template <uint32_t INF> __device__ __forceinline__ uint32_t ord16(uint32_t u) {
 
 // One pixel of the lane kernel: C channel values of one pixel through Io (load(c): raw bits of
 // channel c < C, the loads of a chunk issued before any use; raw(c): the same, re-read; opaque(v): v
-// in a VGPR, hidden from the compiler's scalar analysis; barrier(): a scheduling barrier), the lane's
-// LDS column col (C + 1 words at stride 64) -> the std, the median's and the mode's channels.  The
+// in a VGPR, hidden from the compiler's scalar analysis; pack(lo, hi): two 16-bit images in one
+// register, where it stands; barrier(): a scheduling barrier), the lane's LDS column col (C + 1
+// 16-bit elements at stride 64) -> the std, the median's and the mode's channels.  The
 // kernel passes device memory accessors; tests/native/chanpool_lane_host.cpp runs this same function
 // on the host against the oracle's restatement.
 template <class T, int NP, class Io>
-__device__ __forceinline__ void lane_pixel(Io& io, uint32_t* col, int C, int depth_limit, int exp, float& sd,
+__device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int depth_limit, int exp, float& sd,
                                            int& mi, int& oi) {
-    static_assert(T::bits == 16, "16-bit value images, channel-order keys value << 8 | channel");
+    static_assert(T::bits == 16, "16-bit value images");
     constexpr int H = NP / 2;
-    // loads in chunks of 32 channels, each chunk's loads issued before any use (a scheduling barrier
+    // loads in chunks of 32 channels (the two halves of 16 registers: channels r and r + NP/2), each
+    // chunk's loads issued before any use and its images packed as it lands (a scheduling barrier
     // between chunks keeps 32, not NP, unpacked values in flight); channels past C re-read channel
     // C-1 and are replaced by 0 (the sum) and the all-ones image (the sort: after every value, tied
     // only with NaN, which the scans below stop short of by counting positions < C).  As a chunk
-    // lands: the value images into the packed registers and the channel-order keys (image << 8 |
-    // channel) into the lane's LDS column.  C goes through a VGPR copy (opaque to the compiler) so
+    // lands: the value images into the packed registers and, in channel order, into the lane's LDS
+    // column.  C goes through a VGPR copy (opaque to the compiler) so
     // that the per-channel padding tests are vector arithmetic: as scalar masks, all NP of them were
     // kept live at once and spilled.
     const int Cv = io.opaque(C);
     u16x2 v[H];
 #pragma unroll
-    for (int c0 = 0; c0 < NP; c0 += 32) {
+    for (int r0 = 0; r0 < H; r0 += 16) {  // a chunk: registers r0 .. r0+15, channels r and r + H of each
         uint32_t raw[32];
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            raw[i] = io.load(min(c0 + i, C - 1));
-        }
+        for (int i = 0; i < 32; ++i) raw[i] = io.load(min(r0 + (i & 15) + (i >> 4) * H, C - 1));
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
-            const int c = c0 + i;
+            const int c = r0 + (i & 15) + (i >> 4) * H;
             const uint32_t keep = ~(uint32_t)((Cv - 1 - c) >> 31);  // all ones for c < C
             const uint32_t u = raw[i] & keep;
             const uint32_t o = ord16<T::inf>(u) | (~keep & 0xFFFFu);
-            col[min(c, Cv) * 64] = (o << 8) | (uint32_t)c;  // padding: into the spare word C
-            if (c < H) v[c % H].x = (unsigned short)o;
-            else v[c % H].y = (unsigned short)o;
+            col[min(c, Cv) * 64] = (uint16_t)o;  // padding: into the spare element C
+            raw[i] = o;
         }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[r0 + i] = io.pack(raw[i], raw[i + 16]);
         io.barrier();
     }
+    // the sort right behind the loads: placed after the std passes, the images were packed only
+    // there and all NP of them stayed unpacked (one register each) through those loops
+    if (!(exp & 8)) pk_bitonic<NP>(v);
+    io.barrier();
     // std: two passes in fp64, channel order (as the wave kernel), over the keys in LDS, 8 reads in
     // flight (in the load loop, the fp64 sum held that chunk's values and doubled the registers).  The
     // image inverts to the value bits but for -0 -> +0 (no effect on the sums) and one NaN for all: a
     // column holding NaN (its first one noted here, for the median rule) re-reads its values from
     // global memory instead, so the NaN that propagates is the one the wave kernel's sum carried.
-    auto value = [](uint32_t e) {
-        const uint32_t o = e >> 8;
+    auto value = [](uint32_t o) {
         return (double)T::to_f((o & 0x8000u) ? (o ^ 0x8000u) : (~o & 0xFFFFu));
     };
     double s = 0.0;
     int nanc = -1;
     if (!(exp & 2)) for_channels(col, 0, C, [&](int c, uint32_t e) {
         s += value(e);
-        nanc = (nanc < 0 && (e >> 8) == 0xFFFEu) ? c : nanc;
+        nanc = (nanc < 0 && e == 0xFFFEu) ? c : nanc;
     });
     double m2 = 0.0;
     if (exp & 2) {
@@ -235,8 +253,6 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint32_t* col, int C, int dep
         }
     }
     sd = (float)sqrt(m2 / (double)(C - 1));  // C == 1: NaN, as the reference
-    if (!(exp & 8)) pk_bitonic<NP>(v);
-    io.barrier();
 
     // sorted scan: the median image (position (C-1)/2) and where its run starts; the first longest run
     // of values (the padding's run of 0xFFFF images, after every value, never counts)
@@ -267,7 +283,6 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint32_t* col, int C, int dep
     int seen = 0;
     const int jm = mpos - r0;
     if (!(exp & 4)) for_channels(col, 0, C, [&](int c, uint32_t e) {
-        e >>= 8;
         mi = (e == medv && seen == jm) ? c : mi;
         seen += e == medv ? 1 : 0;
         oi = e == mvl ? c : oi;
@@ -276,22 +291,28 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint32_t* col, int C, int dep
 
     // oi so far: a unique value, or C <= 16 (only the stable insertion sort)
     if (lmax > 1 && C > 16 && !(exp & 1)) {
-        // follow the rightmost introsort range holding two or more mode-valued elements
+        // follow the rightmost introsort range holding two or more mode-valued elements, each carrying
+        // its channel as a code (ModeCode)
+        using MC = ModeCode<T>;
+        for_channels(col, 0, C, [&](int c, uint32_t e) {
+            if (e == mvl) col[c * 64] = (uint16_t)MC::enc(c);
+        });
+        auto val = [mvl](uint32_t e) { return MC::is(e) ? mvl : e; };
         const int lg = 31 - __builtin_clz((unsigned)C);
         int f = 0, l = C, cnt = (int)lmax, depth = depth_limit < 0 ? 2 * lg : depth_limit;
         for (;;) {
             if (cnt == 1 || l - f <= 16 || depth == 0) {
-                if (cnt != 1 && l - f > 16) heap_sort_col(col, f, l);
-                int lastp = f;
-                for_channels(col, f, l, [&](int p, uint32_t e) { lastp = (e >> 8) == mvl ? p : lastp; });
-                oi = (int)(col[lastp * 64] & 0xFF);
+                if (cnt != 1 && l - f > 16) heap_sort_col(col, f, l, val);
+                uint32_t last = 0;  // the range's last mode-valued element (the final insertion sort is stable)
+                for_channels(col, f, l, [&](int, uint32_t e) { last = MC::is(e) ? e : last; });
+                oi = MC::chan(last);
                 break;
             }
             --depth;
             // __move_median_to_first(f, f + 1, mid, l - 1)
             const int mid = f + (l - f) / 2;
             const uint32_t kf = col[f * 64], ka = col[(f + 1) * 64], kb = col[mid * 64], kc = col[(l - 1) * 64];
-            const uint32_t va = ka >> 8, vb = kb >> 8, vc = kc >> 8;
+            const uint32_t va = val(ka), vb = val(kb), vc = val(kc);
             int sel;
             uint32_t ks;
             if (va < vb) {
@@ -301,53 +322,60 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint32_t* col, int C, int dep
                 sel = va < vc ? f + 1 : (vb < vc ? l - 1 : mid);
                 ks = va < vc ? ka : (vb < vc ? kc : kb);
             }
-            col[f * 64] = ks;
-            col[sel * 64] = kf;
-            // __unguarded_partition(f + 1, l, pivot f) as one flat loop over chunks of four positions: a
-            // step reads the next four of the left scan (state 0, ascending from i) or of the right scan
-            // (state 1, descending from j) and takes the first stop among them, so one LDS round trip
-            // covers up to four elements.  Reads past a stop are clamped into the column ([0, C]) and
-            // never used: the median-of-three leaves a stop inside [f, l) for either scan.
-            const uint32_t pv = ks >> 8;
+            col[f * 64] = (uint16_t)ks;
+            col[sel * 64] = (uint16_t)kf;
+            // __unguarded_partition(f + 1, l, pivot f) with both scans advancing at once: in a step the
+            // left scan (ascending from i, stops at a value >= pivot) and the right scan (descending
+            // from j, stops at a value <= pivot) each read their next four positions -- one LDS round
+            // trip -- unless already holding their stop; with both stops held, the pair is swapped
+            // (i < j) or the partition ends at i.  A round's two scans read positions no swap of that
+            // round has touched yet, so running them side by side reads what the sequential algorithm
+            // reads.  Reads are clamped into the column ([0, C]) and never used past a stop: the
+            // median-of-three leaves a stop inside [f, l) for either scan.  Branch-free but for the
+            // loop exit: a step that swaps nothing writes its two elements to the spare element C.
+            const uint32_t pv = val(ks);
             int i = f + 1, j = l - 1;
-            bool rs = false;
-            uint32_t ai = 0;
+            bool lf = false, rf = false;
+            uint32_t ai = 0, bj = 0;
             for (;;) {
-                uint32_t e[4];
+                uint32_t el[4], er[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) e[k] = col[(rs ? max(j - k, 0) : min(i + k, C)) * 64];
-                if (!rs) {
-                    int k = 4;
-#pragma unroll
-                    for (int q = 3; q >= 0; --q) k = (e[q] >> 8) >= pv ? q : k;
-                    i += k;
-                    if (k < 4) {
-                        ai = e[0];
-#pragma unroll
-                        for (int q = 1; q < 4; ++q) ai = q == k ? e[q] : ai;
-                        rs = true;
-                    }
-                } else {
-                    int k = 4;
-#pragma unroll
-                    for (int q = 3; q >= 0; --q) k = (e[q] >> 8) <= pv ? q : k;
-                    j -= k;
-                    if (k < 4) {
-                        if (!(i < j)) break;
-                        uint32_t bj = e[0];
-#pragma unroll
-                        for (int q = 1; q < 4; ++q) bj = q == k ? e[q] : bj;
-                        col[i * 64] = bj;
-                        col[j * 64] = ai;
-                        ++i;
-                        --j;
-                        rs = false;
-                    }
+                for (int q = 0; q < 4; ++q) {
+                    el[q] = col[min(i + q, C) * 64];
+                    er[q] = col[max(j - q, 0) * 64];
                 }
+                int kl = 4, kr = 4;
+#pragma unroll
+                for (int q = 3; q >= 0; --q) {
+                    kl = val(el[q]) >= pv ? q : kl;
+                    kr = val(er[q]) <= pv ? q : kr;
+                }
+                uint32_t sl = el[0], sr = er[0];
+#pragma unroll
+                for (int q = 1; q < 4; ++q) {
+                    sl = kl == q ? el[q] : sl;
+                    sr = kr == q ? er[q] : sr;
+                }
+                i += lf ? 0 : kl;
+                j -= rf ? 0 : kr;
+                ai = lf ? ai : sl;
+                bj = rf ? bj : sr;
+                lf = lf || kl < 4;
+                rf = rf || kr < 4;
+                if (lf && rf && !(i < j)) break;
+                const bool sw = lf && rf;
+                col[(sw ? i : C) * 64] = (uint16_t)bj;
+                col[(sw ? j : C) * 64] = (uint16_t)ai;
+                i += sw ? 1 : 0;
+                j -= sw ? 1 : 0;
+                lf = lf && !sw;
+                rf = rf && !sw;
             }
             const int cut = i;
-            int cr = 0;
-            for_channels(col, cut, l, [&](int, uint32_t e) { cr += (e >> 8) == mvl ? 1 : 0; });
+            // the left part holds values <= pivot, the right part values >= pivot: mode elements
+            // split between the two only when the pivot is the mode value
+            int cr = mvl > pv ? cnt : 0;
+            if (mvl == pv) for_channels(col, cut, l, [&](int, uint32_t e) { cr += MC::is(e) ? 1 : 0; });
             if (cr > 0) {
                 f = cut;
                 cnt = cr;
@@ -356,5 +384,4 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint32_t* col, int C, int dep
             }
         }
     }
-
 }
