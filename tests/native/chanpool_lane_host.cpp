@@ -40,11 +40,11 @@ struct HostIo {
 
 template <class T, int NP>
 static void run(const std::vector<uint16_t>& x, int C, long long npix, int depth, float* sd, int32_t* mi, int32_t* oi) {
-    std::vector<uint16_t> col((size_t)(C + 1) * 64);
+    std::vector<uint16_t> col((size_t)(C + 7) * 64);
     for (long long p = 0; p < npix; ++p) {
         HostIo io{x.data() + p, npix};
         int m, o;
-        lane_pixel<T, NP>(io, col.data(), C, depth, 0, sd[p], m, o);
+        lane_pixel<T, NP>(io, col.data() + 3 * 64, C, depth, 0, sd[p], m, o);
         mi[p] = m;
         oi[p] = o;
     }

@@ -179,8 +179,9 @@ template <uint32_t INF> __device__ __forceinline__ uint32_t ord16(uint32_t u) {
 // One pixel of the lane kernel: C channel values of one pixel through Io (load(c): raw bits of
 // channel c < C, the loads of a chunk issued before any use; raw(c): the same, re-read; opaque(v): v
 // in a VGPR, hidden from the compiler's scalar analysis; pack(lo, hi): two 16-bit images in one
-// register, where it stands; barrier(): a scheduling barrier), the lane's LDS column col (C + 1
-// 16-bit elements at stride 64) -> the std, the median's and the mode's channels.  The
+// register, where it stands; barrier(): a scheduling barrier), the lane's LDS column col (16-bit
+// elements at stride 64, addressable from position -3 to C + 3; C is a spare element) -> the std,
+// the median's and the mode's channels.  The
 // kernel passes device memory accessors; tests/native/chanpool_lane_host.cpp runs this same function
 // on the host against the oracle's restatement.
 template <class T, int NP, class Io>
@@ -330,8 +331,9 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int dep
             // trip -- unless already holding their stop; with both stops held, the pair is swapped
             // (i < j) or the partition ends at i.  A round's two scans read positions no swap of that
             // round has touched yet, so running them side by side reads what the sequential algorithm
-            // reads.  Reads are clamped into the column ([0, C]) and never used past a stop: the
-            // median-of-three leaves a stop inside [f, l) for either scan.  Branch-free but for the
+            // reads.  Reads run at most three positions past a stop (the column is addressable from -3
+            // to C + 3) and are never used there: the median-of-three leaves a stop inside [f, l) for
+            // either scan.  Branch-free but for the
             // loop exit: a step that swaps nothing writes its two elements to the spare element C.
             const uint32_t pv = val(ks);
             int i = f + 1, j = l - 1;
@@ -341,8 +343,8 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int dep
                 uint32_t el[4], er[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    el[q] = col[min(i + q, C) * 64];
-                    er[q] = col[max(j - q, 0) * 64];
+                    el[q] = col[(i + q) * 64];
+                    er[q] = col[(j - q) * 64];
                 }
                 int kl = 4, kr = 4;
 #pragma unroll
