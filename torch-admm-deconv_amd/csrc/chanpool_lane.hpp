@@ -103,12 +103,12 @@ template <int NP> __device__ __forceinline__ void pk_bitonic(u16x2 (&v)[NP / 2])
 // rewritten as channel codes -- images no value takes, so an element carries its channel through the
 // partitions and still compares as the mode value: below the image of -inf (the negative NaN bit
 // patterns, which ord16 folds onto 0xFFFE) and 0x7FFF (-0, folded onto +0).  bf16: codes 0..126 and
-// 0x7FFF for channel 127; f16: codes 0..1022.
-template <class T> struct ModeCode {
+// 0x7FFF for channel 127 (WIDE); f16: codes 0..1022.
+template <class T, bool WIDE> struct ModeCode {
     static constexpr uint32_t lim = T::inf == 0x7F80u ? 0x7Fu : 0x3FFu;
-    __device__ static uint32_t enc(int c) { return (uint32_t)c < lim ? (uint32_t)c : 0x7FFFu; }
-    __device__ static bool is(uint32_t e) { return e < lim || e == 0x7FFFu; }
-    __device__ static int chan(uint32_t e) { return e == 0x7FFFu ? 127 : (int)e; }
+    __device__ static uint32_t enc(int c) { return WIDE && (uint32_t)c >= lim ? 0x7FFFu : (uint32_t)c; }
+    __device__ static bool is(uint32_t e) { return e < lim || (WIDE && e == 0x7FFFu); }  // one compare unless WIDE
+    __device__ static int chan(uint32_t e) { return WIDE && e == 0x7FFFu ? 127 : (int)e; }
 };
 
 // std::__adjust_heap / __push_heap / heap sort on the lane's LDS column, compared by value (val:
@@ -174,6 +174,106 @@ template <uint32_t INF> __device__ __forceinline__ uint32_t ord16(uint32_t u) {
     const uint32_t o = (u ^ ((0u - (u >> 15)) | 0x8000u)) & 0xFFFFu;
     const uint32_t m = 0u - ((INF - t) >> 31);       // all ones for NaN
     return (o & ~m) | (0xFFFEu & m);
+}
+
+// The mode's channel when the introsort reaches it: follow the rightmost range holding two or more
+// mode-valued elements (lmax of them, value image mvl) through libstdc++'s partitions, each carrying
+// its channel as a code (ModeCode).  WIDE: a bf16 column of 128 channels (channel 127's code).
+template <class T, bool WIDE>
+__device__ __forceinline__ int introsort_trace(uint16_t* col, int C, int lmax, uint32_t mvl, int depth_limit) {
+    using MC = ModeCode<T, WIDE>;
+    int oi = 0;
+    for_channels(col, 0, C, [&](int c, uint32_t e) {
+        if (e == mvl) col[c * 64] = (uint16_t)MC::enc(c);
+    });
+    auto val = [mvl](uint32_t e) { return MC::is(e) ? mvl : e; };
+    const int lg = 31 - __builtin_clz((unsigned)C);
+    int f = 0, l = C, cnt = (int)lmax, depth = depth_limit < 0 ? 2 * lg : depth_limit;
+    for (;;) {
+        if (cnt == 1 || l - f <= 16 || depth == 0) {
+            if (cnt != 1 && l - f > 16) heap_sort_col(col, f, l, val);
+            uint32_t last = 0;  // the range's last mode-valued element (the final insertion sort is stable)
+            for_channels(col, f, l, [&](int, uint32_t e) { last = MC::is(e) ? e : last; });
+            oi = MC::chan(last);
+            break;
+        }
+        --depth;
+        // __move_median_to_first(f, f + 1, mid, l - 1)
+        const int mid = f + (l - f) / 2;
+        const uint32_t kf = col[f * 64], ka = col[(f + 1) * 64], kb = col[mid * 64], kc = col[(l - 1) * 64];
+        const uint32_t va = val(ka), vb = val(kb), vc = val(kc);
+        int sel;
+        uint32_t ks;
+        if (va < vb) {
+            sel = vb < vc ? mid : (va < vc ? l - 1 : f + 1);
+            ks = vb < vc ? kb : (va < vc ? kc : ka);
+        } else {
+            sel = va < vc ? f + 1 : (vb < vc ? l - 1 : mid);
+            ks = va < vc ? ka : (vb < vc ? kc : kb);
+        }
+        col[f * 64] = (uint16_t)ks;
+        col[sel * 64] = (uint16_t)kf;
+        // __unguarded_partition(f + 1, l, pivot f) with both scans advancing at once: in a step the
+        // left scan (ascending from i, stops at a value >= pivot) and the right scan (descending
+        // from j, stops at a value <= pivot) each read their next four positions -- one LDS round
+        // trip -- unless already holding their stop; with both stops held, the pair is swapped
+        // (i < j) or the partition ends at i.  A round's two scans read positions no swap of that
+        // round has touched yet, so running them side by side reads what the sequential algorithm
+        // reads.  Reads run at most three positions past a stop (the column is addressable from -3
+        // to C + 3) and are never used there: the median-of-three leaves a stop inside [f, l) for
+        // either scan.  Branch-free but for the
+        // loop exit: a step that swaps nothing writes its two elements to the spare element C.
+        const uint32_t pv = val(ks);
+        int i = f + 1, j = l - 1;
+        bool lf = false, rf = false;
+        uint32_t ai = 0, bj = 0;
+        for (;;) {
+            uint32_t el[4], er[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                el[q] = col[(i + q) * 64];
+                er[q] = col[(j - q) * 64];
+            }
+            int kl = 4, kr = 4;
+#pragma unroll
+            for (int q = 3; q >= 0; --q) {
+                kl = val(el[q]) >= pv ? q : kl;
+                kr = val(er[q]) <= pv ? q : kr;
+            }
+            uint32_t sl = el[0], sr = er[0];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                sl = kl == q ? el[q] : sl;
+                sr = kr == q ? er[q] : sr;
+            }
+            i += lf ? 0 : kl;
+            j -= rf ? 0 : kr;
+            ai = lf ? ai : sl;
+            bj = rf ? bj : sr;
+            lf = lf || kl < 4;
+            rf = rf || kr < 4;
+            if (lf && rf && !(i < j)) break;
+            const bool sw = lf && rf;
+            col[(sw ? i : C) * 64] = (uint16_t)bj;
+            col[(sw ? j : C) * 64] = (uint16_t)ai;
+            i += sw ? 1 : 0;
+            j -= sw ? 1 : 0;
+            lf = lf && !sw;
+            rf = rf && !sw;
+        }
+        const int cut = i;
+        // the left part holds values <= pivot, the right part values >= pivot: mode elements
+        // split between the two only when the pivot is the mode value
+        int cr = mvl > pv ? cnt : 0;
+        if (mvl == pv) for_channels(col, cut, l, [&](int, uint32_t e) { cr += MC::is(e) ? 1 : 0; });
+        if (cr > 0) {
+            f = cut;
+            cnt = cr;
+        } else {
+            l = cut;
+        }
+    }
+    return oi;
 }
 
 // One pixel of the lane kernel: C channel values of one pixel through Io (load(c): raw bits of
@@ -291,99 +391,8 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int dep
     if (nanc >= 0) mi = nanc;
 
     // oi so far: a unique value, or C <= 16 (only the stable insertion sort)
-    if (lmax > 1 && C > 16 && !(exp & 1)) {
-        // follow the rightmost introsort range holding two or more mode-valued elements, each carrying
-        // its channel as a code (ModeCode)
-        using MC = ModeCode<T>;
-        for_channels(col, 0, C, [&](int c, uint32_t e) {
-            if (e == mvl) col[c * 64] = (uint16_t)MC::enc(c);
-        });
-        auto val = [mvl](uint32_t e) { return MC::is(e) ? mvl : e; };
-        const int lg = 31 - __builtin_clz((unsigned)C);
-        int f = 0, l = C, cnt = (int)lmax, depth = depth_limit < 0 ? 2 * lg : depth_limit;
-        for (;;) {
-            if (cnt == 1 || l - f <= 16 || depth == 0) {
-                if (cnt != 1 && l - f > 16) heap_sort_col(col, f, l, val);
-                uint32_t last = 0;  // the range's last mode-valued element (the final insertion sort is stable)
-                for_channels(col, f, l, [&](int, uint32_t e) { last = MC::is(e) ? e : last; });
-                oi = MC::chan(last);
-                break;
-            }
-            --depth;
-            // __move_median_to_first(f, f + 1, mid, l - 1)
-            const int mid = f + (l - f) / 2;
-            const uint32_t kf = col[f * 64], ka = col[(f + 1) * 64], kb = col[mid * 64], kc = col[(l - 1) * 64];
-            const uint32_t va = val(ka), vb = val(kb), vc = val(kc);
-            int sel;
-            uint32_t ks;
-            if (va < vb) {
-                sel = vb < vc ? mid : (va < vc ? l - 1 : f + 1);
-                ks = vb < vc ? kb : (va < vc ? kc : ka);
-            } else {
-                sel = va < vc ? f + 1 : (vb < vc ? l - 1 : mid);
-                ks = va < vc ? ka : (vb < vc ? kc : kb);
-            }
-            col[f * 64] = (uint16_t)ks;
-            col[sel * 64] = (uint16_t)kf;
-            // __unguarded_partition(f + 1, l, pivot f) with both scans advancing at once: in a step the
-            // left scan (ascending from i, stops at a value >= pivot) and the right scan (descending
-            // from j, stops at a value <= pivot) each read their next four positions -- one LDS round
-            // trip -- unless already holding their stop; with both stops held, the pair is swapped
-            // (i < j) or the partition ends at i.  A round's two scans read positions no swap of that
-            // round has touched yet, so running them side by side reads what the sequential algorithm
-            // reads.  Reads run at most three positions past a stop (the column is addressable from -3
-            // to C + 3) and are never used there: the median-of-three leaves a stop inside [f, l) for
-            // either scan.  Branch-free but for the
-            // loop exit: a step that swaps nothing writes its two elements to the spare element C.
-            const uint32_t pv = val(ks);
-            int i = f + 1, j = l - 1;
-            bool lf = false, rf = false;
-            uint32_t ai = 0, bj = 0;
-            for (;;) {
-                uint32_t el[4], er[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    el[q] = col[(i + q) * 64];
-                    er[q] = col[(j - q) * 64];
-                }
-                int kl = 4, kr = 4;
-#pragma unroll
-                for (int q = 3; q >= 0; --q) {
-                    kl = val(el[q]) >= pv ? q : kl;
-                    kr = val(er[q]) <= pv ? q : kr;
-                }
-                uint32_t sl = el[0], sr = er[0];
-#pragma unroll
-                for (int q = 1; q < 4; ++q) {
-                    sl = kl == q ? el[q] : sl;
-                    sr = kr == q ? er[q] : sr;
-                }
-                i += lf ? 0 : kl;
-                j -= rf ? 0 : kr;
-                ai = lf ? ai : sl;
-                bj = rf ? bj : sr;
-                lf = lf || kl < 4;
-                rf = rf || kr < 4;
-                if (lf && rf && !(i < j)) break;
-                const bool sw = lf && rf;
-                col[(sw ? i : C) * 64] = (uint16_t)bj;
-                col[(sw ? j : C) * 64] = (uint16_t)ai;
-                i += sw ? 1 : 0;
-                j -= sw ? 1 : 0;
-                lf = lf && !sw;
-                rf = rf && !sw;
-            }
-            const int cut = i;
-            // the left part holds values <= pivot, the right part values >= pivot: mode elements
-            // split between the two only when the pivot is the mode value
-            int cr = mvl > pv ? cnt : 0;
-            if (mvl == pv) for_channels(col, cut, l, [&](int, uint32_t e) { cr += MC::is(e) ? 1 : 0; });
-            if (cr > 0) {
-                f = cut;
-                cnt = cr;
-            } else {
-                l = cut;
-            }
-        }
-    }
+    if (lmax > 1 && C > 16 && !(exp & 1))
+        oi = (ModeCode<T, false>::lim <= 0x7Fu && C > (int)ModeCode<T, false>::lim)
+                 ? introsort_trace<T, true>(col, C, (int)lmax, mvl, depth_limit)
+                 : introsort_trace<T, false>(col, C, (int)lmax, mvl, depth_limit);
 }
