@@ -63,7 +63,10 @@ typedef void (*admm_tv_allreduce_fn)(float* buf, size_t count, void* stream, voi
  * sequence -- the two ADMMDeconv modules of DivergentAttention's first level
  * (blocks.py:187-196).  out / gout / history then hold G*B*C planes (module-major),
  * glam / grho G values, gxin the sum over modules.  Each module's iso norm runs over its
- * own (B,C).  Fused power-of-two sizes only, no PSF gradient.
+ * own (B,C).  No PSF gradient.  Power-of-two sizes: every launch covers all modules' planes
+ * (inference and training); smooth sizes (admm_tv_supported == 3): the modules are solved one
+ * after another inside the call, sharing b = H_t(xin) and the tables -- inference only
+ * (training entry points return ADMM_TV_EUNSUPPORTED there: one call per module).
  *
  * allreduce / allreduce_ctx: the per-call cross-rank hook above (NULL: single process;
  * ignored for iso = 0).  Everything a call needs is in its arguments: the library keeps no

@@ -1,7 +1,9 @@
 """Grouped solves (desc.groups): G modules sharing the input, own lambda / rho,
 one native pass sequence.  Must equal G separate fft_admm_tv calls: aniso bit for bit (every
 plane's arithmetic is the same), iso to fp32 reassociation (the per-module norm sums planes in
-different group sizes), gradients likewise (lambda / rho per module, x summed over modules)."""
+different group sizes), gradients likewise (lambda / rho per module, x summed over modules).
+Power-of-two sizes run the modules in every launch; smooth sizes (720x1280, 240x480) one module
+after another inside one call (inference)."""
 import pytest
 import torch
 
@@ -15,7 +17,11 @@ def rel(a, b):
 
 @pytest.mark.parametrize("iso,psf,shape", [(False, None, (2, 3, 64, 128)), (True, None, (4, 3, 64, 64)),
                                            (False, ("gauss:1.0", 5), (1, 3, 128, 64)),
-                                           (True, ("motion", 7), (2, 2, 32, 256))])
+                                           (True, ("motion", 7), (2, 2, 32, 256)),
+                                           # smooth sizes (mixed-radix kernels): inference grouped in one
+                                           # call, training one call per module
+                                           (False, ("gauss:1.5", 9), (2, 3, 720, 1280)),
+                                           (True, ("motion", 7), (2, 3, 240, 480))])
 def test_grouped_equals_separate(cuda_dev, iso, psf, shape):
     from admmtor.eops.deconv import fft_admm_tv, fft_admm_tv_grouped
     from admmtor.synth import blurred_batch, make_psf

@@ -252,8 +252,11 @@ def fft_admm_tv_grouped(xin: torch.Tensor, lmbds, rhos, kern: torch.Tensor, iso:
     call (desc.groups = G): every launch covers all modules' planes, each module keeps its own
     Wiener factor (its rho) and, for iso, its own per-pixel norm over its (B, C).  This is how
     DivergentAttention's ADMM modules that share x run (blocks.py:187-196).
-    Autograd reaches xin (summed over modules) and every lambda / rho.  Needs power-of-two
-    H, W on the fused kernels and a PSF that does not require grad; returns G tensors.
+    Autograd reaches xin (summed over modules) and every lambda / rho.  Power-of-two H, W run
+    on the fused kernels (inference and training); smooth sizes (``admm_tv_supported == 3``)
+    solve the modules one after another inside one native call on the mixed-radix kernels,
+    sharing b = H_t(xin) and the tables (inference), and train as one call per module.  The PSF
+    must not require grad; returns G tensors.
     """
     if not isinstance(kern, torch.Tensor):
         kern = torch.as_tensor(kern)
@@ -265,12 +268,16 @@ def fft_admm_tv_grouped(xin: torch.Tensor, lmbds, rhos, kern: torch.Tensor, iso:
     if G != len(rhos) or G < 1:
         raise ValueError("lmbds and rhos must have the same, non-zero length")
     B, C, H, W = xin.shape
-    if _native.load().admm_tv_supported(H, W) != 1 or (kern.requires_grad and kern.numel() > 0):
-        raise NotImplementedError("grouped solve: power-of-two H, W (fused kernels) and a fixed PSF only")
+    sup = _native.load().admm_tv_supported(H, W)
+    if sup not in (1, 3) or (kern.requires_grad and kern.numel() > 0):
+        raise NotImplementedError("grouped solve: power-of-two or smooth H, W and a fixed PSF only")
     maxit = max(0, int(maxit))
     dev = xin.device
     needs_grad = torch.is_grad_enabled() and (
         xin.requires_grad or any(isinstance(v, torch.Tensor) and v.requires_grad for v in (*lmbds, *rhos)))
+    if needs_grad and sup == 3:
+        # grouped training is power-of-two only (include/admm_tv.h): one training call per module
+        return [fft_admm_tv(xin, l, r, kern, iso, maxit) for l, r in zip(lmbds, rhos)]
     if needs_grad:
         # lambda and rho stacked into (G,) tensors differentiably, so each module's parameters get theirs
         x32 = xin.to(torch.float32).contiguous()

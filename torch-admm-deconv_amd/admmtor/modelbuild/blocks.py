@@ -136,7 +136,7 @@ class DivergentAttention(nn.Module):
                              for m in mods))
         if groupable:
             from admmtor import _native
-            groupable = _native.load().admm_tv_supported(x.shape[-2], x.shape[-1]) == 1
+            groupable = _native.load().admm_tv_supported(x.shape[-2], x.shape[-1]) in (1, 3)
         if not groupable:
             return [m(x) for m in mods]
         sols = fft_admm_tv_grouped(x, [m.lmbda for m in mods], [m.rho for m in mods], mods[0].w,

@@ -210,8 +210,8 @@ Layout make_layout(const admm_tv_desc& d) {
         L.mm = mm_plan((int)H, (int)W);
         L.mmr = mm_plan_row((int)W);
     }
-    L.mixed = L.gen && !f64 && G == 1 && mixed_hw(d.H, d.W);
-    L.mixed_train = L.mixed && !(k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD));
+    L.mixed = L.gen && !f64 && mixed_hw(d.H, d.W) && (G == 1 || !(d.flags & ADMM_TV_FLAG_PSF_GRAD));
+    L.mixed_train = L.mixed && G == 1 && !(k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD));
     L.odd = L.gen && !f64 && G == 1 && !d.iso && odd_hw(d.H, d.W);
     L.ldw = (int)(N + 1);
     if (L.gen && !f64 && L.mm.ok && L.mmr.ok && env_int("ADMM_GEN_PITCH", 1)) L.ldw = (int)((N + 1 + 15) / 16 * 16);
@@ -234,7 +234,7 @@ Layout make_layout(const admm_tv_desc& d) {
     L.twHd = take(H * sizeof(double2));
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
     L.gscr = L.gen ? take(glb_scratch((int)H, (int)W, (long long)P, f64)) : 0;
-    L.fcM = L.mixed ? take((2 * N + 1) * H * sizeof(float)) : 0;  // [H][N + 1] + packed copy, k_fc_mixed
+    L.fcM = L.mixed ? take(G * (2 * N + 1) * H * sizeof(float)) : 0;  // per module: [H][N + 1] + packed copy, k_fc_mixed
     L.spec2 = L.odd ? take(P * H * (size_t)L.ldw * csz) : 0;
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
@@ -563,6 +563,14 @@ int xspec(int H, const cf* U, const cf* V, cf* part, const cf* twH, int N, int P
     }
 }
 
+// grouped modules train only on the fused power-of-two path (a smooth size solves them one after
+// another for inference only; training there takes one call per module)
+int grouped_train_check(const admm_tv_desc& d) {
+    if (d.groups > 1 && !supported_hw(d.H, d.W))
+        return fail(ADMM_TV_EUNSUPPORTED, "grouped training needs power-of-two H, W: one call per module");
+    return 0;
+}
+
 int validate(const admm_tv_desc* d) {
     if (!d) return fail(ADMM_TV_EINVAL, "null descriptor");
     const bool empty_ok = d->iso && d->allreduce && d->B >= 0 && d->C >= 0;  // see participate_only
@@ -574,8 +582,8 @@ int validate(const admm_tv_desc* d) {
         return fail(ADMM_TV_EUNSUPPORTED, "unsupported H, W (admm_tv_supported / admm_tv_supported_f64: up to 65,536)");
     if (is_f64(*d) && d->groups > 1) return fail(ADMM_TV_EUNSUPPORTED, "groups > 1: fp32 only");
     if (d->kh > d->H || d->kw > d->W) return fail(ADMM_TV_EKERNEL, "PSF larger than the image");
-    if (d->groups > 1 && (!supported_hw(d->H, d->W) || (d->flags & ADMM_TV_FLAG_PSF_GRAD)))
-        return fail(ADMM_TV_EUNSUPPORTED, "groups > 1 needs power-of-two H, W and no PSF gradient");
+    if (d->groups > 1 && ((!supported_hw(d->H, d->W) && !mixed_hw(d->H, d->W)) || (d->flags & ADMM_TV_FLAG_PSF_GRAD)))
+        return fail(ADMM_TV_EUNSUPPORTED, "groups > 1 needs power-of-two or smooth H, W and no PSF gradient");
     return 0;
 }
 
@@ -624,11 +632,12 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const T* kern, cons
                 if (int e = launch_check("k_fc_pack")) return e;
             }
             if constexpr (std::is_same<T, float>::value) if (Lo.mixed) {
-                hipError_t e = admm_mixed::fc_mixed(at<float>(ws, Lo.fcT), at<float>(ws, Lo.fcM), H, N, s);
+                hipError_t e = admm_mixed::fc_mixed(at<float>(ws, Lo.fcT) + (size_t)g * n,
+                                                    at<float>(ws, Lo.fcM) + (size_t)g * (2 * N + 1) * H, H, N, s);
                 if (e != hipSuccess) return fail(ADMM_TV_EHIP, std::string("k_fc_mixed: ") + hipGetErrorString(e));
             }
-            if constexpr (std::is_same<T, float>::value) if (Lo.gen && Lo.mm.ok) {
-                float* fc = at<float>(ws, Lo.fcT);  // the generic path has one module
+            if constexpr (std::is_same<T, float>::value) if (Lo.gen && Lo.mm.ok && ngroups_of(d) == 1) {
+                float* fc = at<float>(ws, Lo.fcT);  // the generic path has one module (grouped: the mixed path)
                 hipLaunchKernelGGL(k_fc_transpose, dim3(std::min(4096, (n + nt - 1) / nt)), dim3(nt), 0, s, fc, fc + n, H,
                                    N + 1);
                 if (int e = launch_check("k_fc_transpose")) return e;
@@ -1622,7 +1631,6 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
     const int H = (int)d.H, W = (int)d.W, N = W / 2;
     cf* twW = at<cf>(ws, Lo.twW);
     cf* twH = at<cf>(ws, Lo.twH);
-    const float* fcM = at<float>(ws, Lo.fcM);
     cf* spec[2] = {at<cf>(ws, Lo.spec[0]), at<cf>(ws, Lo.spec[1])};
     float* u[4] = {at<float>(ws, Lo.u[0]), at<float>(ws, Lo.u[1]), at<float>(ws, Lo.u[2]), at<float>(ws, Lo.u[3])};
     auto hchk = [&](hipError_t e, const char* what) {
@@ -1640,6 +1648,19 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
         if (int e = hchk(admm_mixed::r2c(N, bimg, spec[0], twW, rows, s), "k_row_r2c_m")) return e;  // r_1 = b
     }
     const int R = strip_rows_mixed(H, rows, N);
+    // grouped modules (desc.groups, inference only): one module after another through the iteration,
+    // each with its own Wiener factor, lambda, rho and (iso) norm, sharing b and the tables
+    const int G = ngroups_of(d);
+    const int gpm = Lo.ngroups / G;  // iso plane groups per module (a group never straddles two)
+    for (int g = 0; g < G; ++g) {
+    const float* fcM = at<float>(ws, Lo.fcM) + (size_t)g * (2 * N + 1) * H;
+    const float* lamg = lam + g;
+    const float* rhog = rho + g;
+    float* outg = out + (size_t)g * P * H * W;
+    if (g > 0) {  // r_1 = b again: the previous module's iterations overwrote it
+        ProfScope ps(3, s);
+        if (int e = hchk(admm_mixed::r2c(N, bimg, spec[0], twW, rows, s), "k_row_r2c_m")) return e;
+    }
     int cur = 0, uin = 0;
     for (int it = 1; it <= d.maxit; ++it) {
         {
@@ -1648,8 +1669,8 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
         }
         if (it == d.maxit) {
             ProfScope ps(3, s);
-            if (int e = hchk(admm_mixed::c2r(N, spec[cur], out, twW, rows, s), "k_row_c2r_m")) return e;
-            if (!train) return 0;
+            if (int e = hchk(admm_mixed::c2r(N, spec[cur], outg, twW, rows, s), "k_row_c2r_m")) return e;
+            if (!train) break;
         }
         const bool first = it == 1;
         const float *uxi, *uyi, *nprev = nullptr;
@@ -1670,24 +1691,25 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
         if (d.iso) {
             ProfScope ps(2, s);
             float* nout = train ? hn(it) : at<float>(ws, Lo.nsq);
-            IsoArgs ia{spec[cur], uxi, uyi, nprev, lam, rho, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
-                       (long long)Lo.ngroups * H, P};
+            IsoArgs ia{spec[cur], uxi, uyi, nprev, lamg, rhog, at<float>(ws, Lo.part), twW, (int)P, H, Lo.ppg,
+                       (long long)gpm * H, P};
             if (int e = hchk(admm_mixed::iso_norm(N, ia, first, train, s), "k_iso_norm_m")) return e;
             const long long n4 = 2LL * H * W / 4;
             hipLaunchKernelGGL(k_iso_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, at<float4>(ws, Lo.part),
-                               reinterpret_cast<float4*>(nout), Lo.ngroups, n4);
+                               reinterpret_cast<float4*>(nout), gpm, n4);
             if (int e = launch_check("k_iso_reduce")) return e;
             allreduce(d, nout, 2ull * H * W, s);  // sharded batch: sums over every rank's planes
             nsq = nout;
         }
         {
             ProfScope ps(0, s);
-            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, nprev, lam, rho, twW, H, R,
+            PassAArgs pa{spec[cur], spec[1 - cur], bimg, uxi, uyi, uxo, uyo, nsq, nprev, lamg, rhog, twW, H, R,
                          rows / R, P, 0};
             if (int e = hchk(admm_mixed::pass_a(N, pa, d.iso != 0, first, train, s), "k_pass_a_m")) return e;
         }
         cur = 1 - cur;
         uin = 1 - uin;
+    }
     }
     return 0;
 }
@@ -1727,12 +1749,15 @@ int run_forward(const admm_tv_desc& d, const float* xin, const float* kern, cons
         return 0;
     }
     if (participate_only(d)) {  // the same reductions as run_forward's iso loop, contributing zeros
-        const size_t n = (size_t)G * 2 * H * W;
-        for (int it = 1; it <= d.maxit; ++it) {
-            if (it == d.maxit && !hist) break;
-            HIPCHK(hipMemsetAsync(at<float>(ws, Lo.nsq), 0, n * sizeof(float), s));
-            allreduce(d, at<float>(ws, Lo.nsq), Lo.gen ? 2ull * H * W : n, s);
-        }
+        // (grouped modules at a smooth size: one module's iterations after another, 2HW per reduction)
+        const bool by_module = Lo.gen && G > 1;
+        const size_t n = (Lo.gen ? 1 : (size_t)G) * 2 * H * W;
+        for (int g = 0; g < (by_module ? G : 1); ++g)
+            for (int it = 1; it <= d.maxit; ++it) {
+                if (it == d.maxit && !hist) break;
+                HIPCHK(hipMemsetAsync(at<float>(ws, Lo.nsq), 0, n * sizeof(float), s));
+                allreduce(d, at<float>(ws, Lo.nsq), n, s);
+            }
         return 0;
     }
     if (int e = setup(d, Lo, ws, kern, rho, s)) return e;
@@ -2167,6 +2192,9 @@ int admm_tv_supported_f64(int64_t H, int64_t W) { return f64_hw(H, W) ? 1 : 0; }
 
 int admm_tv_path(const admm_tv_desc* d, int train) {
     if (int e = validate(d)) return e;
+    if (train) {
+        if (int e = grouped_train_check(*d)) return e;
+    }
     if (is_f64(*d)) return ADMM_TV_PATH_GENERIC;  // the generic kernels' double instantiation
     const Layout Lo = make_layout(*d);
     if (Lo.tr) return train ? ADMM_TV_PATH_GENERIC : ADMM_TV_PATH_ODD;
@@ -2198,6 +2226,7 @@ int admm_tv_forward(const admm_tv_desc* dp, const float* xin, const float* kern,
 
 int admm_tv_history_size(const admm_tv_desc* d, size_t* bytes) {
     if (int e = validate(d)) return e;
+    if (int e = grouped_train_check(*d)) return e;
     if (!bytes) return fail(ADMM_TV_EINVAL, "null bytes");
     *bytes = make_hist(*d).total;
     return 0;
@@ -2207,6 +2236,7 @@ int admm_tv_forward_train(const admm_tv_desc* dp, const float* xin, const float*
                           const float* rho, float* out, void* hist, size_t hist_bytes, void* ws, size_t ws_bytes,
                           void* stream) {
     if (int e = validate(dp)) return e;
+    if (int e = grouped_train_check(*dp)) return e;
     if (is_f64(*dp)) return fail(ADMM_TV_EINVAL, "ADMM_TV_FLAG_F64: use admm_tv_forward_train_f64");
     if (((!xin || !out) && !participate_only(*dp)) || !lam || !rho || (dp->kh > 0 && !kern))
         return fail(ADMM_TV_EINVAL, "null pointer argument");
@@ -2220,6 +2250,7 @@ int admm_tv_forward_train(const admm_tv_desc* dp, const float* xin, const float*
 
 int admm_tv_backward_workspace_size(const admm_tv_desc* d, size_t* bytes) {
     if (int e = validate(d)) return e;
+    if (int e = grouped_train_check(*d)) return e;
     if (!bytes) return fail(ADMM_TV_EINVAL, "null bytes");
     *bytes = make_bwd_layout(*d).total;
     return 0;
@@ -2229,6 +2260,7 @@ int admm_tv_backward(const admm_tv_desc* dp, const float* xin, const float* kern
                      const float* rho, const float* gout, const void* hist, size_t hist_bytes, float* gxin,
                      float* glam, float* grho, float* gkern, void* ws, size_t ws_bytes, void* stream) {
     if (int e = validate(dp)) return e;
+    if (int e = grouped_train_check(*dp)) return e;
     if (is_f64(*dp)) return fail(ADMM_TV_EINVAL, "ADMM_TV_FLAG_F64: use admm_tv_backward_f64");
     const admm_tv_desc d = *dp;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
