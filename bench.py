@@ -613,10 +613,13 @@ def main():
             print(f"bench rank 0/{world}: {msg}", file=sys.stderr, flush=True)
 
     progress("process group up")
-    # rank-local shard of synthetic blurred images, generated directly in HBM (torch.fft on the device; each
-    # rank has its own rocFFT kernel cache, rocfft_rank_cache)
+    # rank-local shard of synthetic blurred images: in HBM directly at N = 1; with N > 1 synthesised on the
+    # host and copied in, so the ranks run no torch.fft of their own.  Round 6 synthesised on the device
+    # with a rocFFT kernel cache per rank (rocfft_rank_cache, still set): the 8-rank rehearsal passed once,
+    # then stalled again after "inputs generated" with ranks missing at the next collective.
     psf = make_psf(kind, k).to(dev) if k else torch.empty(0, device=dev)
-    x = blurred_batch(B, C, H, W, psf.cpu(), seed=CONFIG_SEED + 2 + 1000 * rank, device=dev)
+    syn_dev = dev if world == 1 else torch.device("cpu")
+    x = blurred_batch(B, C, H, W, psf.cpu(), seed=CONFIG_SEED + 2 + 1000 * rank, device=syn_dev).to(dev)
     lam = torch.tensor([0.01], device=dev)
     rho = torch.tensor([0.02], device=dev)
     torch.cuda.synchronize()

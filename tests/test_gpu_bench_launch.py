@@ -40,12 +40,11 @@ def test_bench_gpus_n_launches_n_ranks(cuda_dev, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [2, 8])
-def test_ranks_synthesise_on_device_after_parent_used_rocfft(cuda_dev, n):
-    """the ranks' first device FFT stalled when the parent process had used rocFFT
-    (its per-user kernel-cache database, held open by the parent).  This parent runs device FFTs of the BSD
-    sizes (run-time compiled Bluestein kernels, written to its cache) and keeps rocFFT loaded; then N
-    rehearsal ranks synthesise their BSD shards with torch.fft on the device, each with its own cache
-    (bench.rocfft_rank_cache), and the run completes."""
+def test_ranks_after_parent_used_rocfft(cuda_dev, n):
+    """the ranks' first device FFT stalled when the parent process had used rocFFT.
+    This parent runs device FFTs of the BSD sizes (run-time compiled Bluestein kernels) and keeps rocFFT
+    loaded; then N rehearsal ranks (each with its own rocFFT cache, bench.rocfft_rank_cache; shards
+    synthesised on the host) solve their BSD shards, and the run completes."""
     import torch
     x = torch.rand(2, 3, 321, 481, device=cuda_dev)
     y = torch.fft.irfftn(torch.fft.rfftn(x, dim=(2, 3)), s=(321, 481), dim=(2, 3))
