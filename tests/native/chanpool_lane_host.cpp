@@ -44,7 +44,7 @@ static void run(const std::vector<uint16_t>& x, int C, long long npix, int depth
     for (long long p = 0; p < npix; ++p) {
         HostIo io{x.data() + p, npix};
         int m, o;
-        lane_pixel<T, NP>(io, col.data() + 3 * 64, C, depth, 0, sd[p], m, o);
+        lane_pixel<T, NP>(io, col.data() + 3 * 64, C, depth, sd[p], m, o);
         mi[p] = m;
         oi[p] = o;
     }

@@ -525,7 +525,7 @@ template <class T, int NP>
 __global__ void __launch_bounds__(64) k_chanpool_lane(const typename T::store* __restrict__ x,
                                                       typename T::store* __restrict__ out,
                                                       int16_t* __restrict__ idx, int C, long long HW,
-                                                      long long npix, int depth_limit, int exp) {
+                                                      long long npix, int depth_limit) {
     using S = typename T::store;
     extern __shared__ __align__(16) uint16_t colmem[];
     const int lane = threadIdx.x;
@@ -542,7 +542,7 @@ __global__ void __launch_bounds__(64) k_chanpool_lane(const typename T::store* _
     io.xp = x + (size_t)b * C * HW + hw;
     float sd;
     int mi, oi;
-    lane_pixel<T, NP>(io, colmem + 3 * 64 + lane, C, depth_limit, exp, sd, mi, oi);  // positions -3 .. C + 3
+    lane_pixel<T, NP>(io, colmem + 3 * 64 + lane, C, depth_limit, sd, mi, oi);  // positions -3 .. C + 3
     const size_t o3 = (size_t)b * 3 * HW + hw;
     out[o3] = (S)T::from_f(sd);
     // the selected elements themselves (-0.0, NaN payloads); the channels clamped into [0, C) for
@@ -608,8 +608,7 @@ int launch_lane(const void* x, int64_t B, int64_t C, int64_t HW, void* out, int1
     const long long npix = (long long)B * HW;
     hipLaunchKernelGGL((k_chanpool_lane<T, NP>), dim3((unsigned)((npix + 63) / 64)), dim3(64),
                        (size_t)(C + 7) * 64 * sizeof(uint16_t), s, static_cast<const typename T::store*>(x),
-                       static_cast<typename T::store*>(out), idx, (int)C, (long long)HW, npix, depth,
-                       env_int("ADMM_CHANPOOL_EXP", 0));  // A/B knob: phases skipped for timing (wrong results)
+                       static_cast<typename T::store*>(out), idx, (int)C, (long long)HW, npix, depth);
     return hipGetLastError() == hipSuccess ? 0 : ADMM_TV_EHIP;
 }
 

@@ -285,7 +285,7 @@ __device__ __forceinline__ int introsort_trace(uint16_t* col, int C, int lmax, u
 // kernel passes device memory accessors; tests/native/chanpool_lane_host.cpp runs this same function
 // on the host against the oracle's restatement.
 template <class T, int NP, class Io>
-__device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int depth_limit, int exp, float& sd,
+__device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int depth_limit, float& sd,
                                            int& mi, int& oi) {
     static_assert(T::bits == 16, "16-bit value images");
     constexpr int H = NP / 2;
@@ -320,7 +320,7 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int dep
     }
     // the sort right behind the loads: placed after the std passes, the images were packed only
     // there and all NP of them stayed unpacked (one register each) through those loops
-    if (!(exp & 8)) pk_bitonic<NP>(v);
+    pk_bitonic<NP>(v);
     io.barrier();
     // std: two passes in fp64, channel order (as the wave kernel), over the keys in LDS, 8 reads in
     // flight (in the load loop, the fp64 sum held that chunk's values and doubled the registers).  The
@@ -332,13 +332,12 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int dep
     };
     double s = 0.0;
     int nanc = -1;
-    if (!(exp & 2)) for_channels(col, 0, C, [&](int c, uint32_t e) {
+    for_channels(col, 0, C, [&](int c, uint32_t e) {
         s += value(e);
         nanc = (nanc < 0 && e == 0xFFFEu) ? c : nanc;
     });
     double m2 = 0.0;
-    if (exp & 2) {
-    } else if (nanc < 0) {
+    if (nanc < 0) {
         const double mean = s / (double)C;
         for_channels(col, 0, C, [&](int, uint32_t e) {
             const double d = value(e) - mean;
@@ -383,7 +382,7 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int dep
     oi = 0;
     int seen = 0;
     const int jm = mpos - r0;
-    if (!(exp & 4)) for_channels(col, 0, C, [&](int c, uint32_t e) {
+    for_channels(col, 0, C, [&](int c, uint32_t e) {
         mi = (e == medv && seen == jm) ? c : mi;
         seen += e == medv ? 1 : 0;
         oi = e == mvl ? c : oi;
@@ -391,7 +390,7 @@ __device__ __forceinline__ void lane_pixel(Io& io, uint16_t* col, int C, int dep
     if (nanc >= 0) mi = nanc;
 
     // oi so far: a unique value, or C <= 16 (only the stable insertion sort)
-    if (lmax > 1 && C > 16 && !(exp & 1))
+    if (lmax > 1 && C > 16)
         oi = (ModeCode<T, false>::lim <= 0x7Fu && C > (int)ModeCode<T, false>::lim)
                  ? introsort_trace<T, true>(col, C, (int)lmax, mvl, depth_limit)
                  : introsort_trace<T, false>(col, C, (int)lmax, mvl, depth_limit);
