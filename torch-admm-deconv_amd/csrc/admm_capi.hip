@@ -158,6 +158,7 @@ size_t up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Layout {
     size_t spec[2], u[4], b, fcT, mT, twW, twH, twHd, G, part, nsq, sigma, total;
+    size_t mM;  // mixed path with a PSF: the multiplier for b = H_t(xin) on the mixed transforms (mt_mixed)
     // generic path: the matrix-core plans, decided once per call (their environment knobs are read
     // here only, so the regions sized below and the kernels launched later always agree)
     MMPlan mm, mmr;
@@ -235,6 +236,7 @@ Layout make_layout(const admm_tv_desc& d) {
     L.G = take((size_t)(k > 0 ? k : 1) * (N + 1) * sizeof(double2));
     L.gscr = L.gen ? take(glb_scratch((int)H, (int)W, (long long)P, f64)) : 0;
     L.fcM = L.mixed ? take(G * (2 * N + 1) * H * sizeof(float)) : 0;  // per module: [H][N + 1] + packed copy, k_fc_mixed
+    L.mM = (L.mixed && k > 0) ? take((N + 1) * H * 2 * sizeof(float)) : 0;
     L.spec2 = L.odd ? take(P * H * (size_t)L.ldw * csz) : 0;
     L.sigma = (k > 0 && (d.flags & ADMM_TV_FLAG_PSF_GRAD)) ? take((N + 1) * H * sizeof(double2)) : 0;
     if (d.iso) {
@@ -642,6 +644,10 @@ int setup(const admm_tv_desc& d, const Layout& Lo, void* ws, const T* kern, cons
                                    N + 1);
                 if (int e = launch_check("k_fc_transpose")) return e;
             }
+        }
+        if constexpr (std::is_same<T, float>::value) if (Lo.mixed && k > 0) {
+            hipError_t e = admm_mixed::mt_mixed(at<cf>(ws, Lo.mT), at<cf>(ws, Lo.mM), H, N, s);
+            if (e != hipSuccess) return fail(ADMM_TV_EHIP, std::string("k_mt_mixed: ") + hipGetErrorString(e));
         }
     }
     return 0;
@@ -1640,9 +1646,19 @@ int run_forward_mixed(const admm_tv_desc& d, const Layout& Lo, const float* xin,
     const float* bimg = xin;
     {
         ProfScope ps(3, s);
-        if (d.kh > 0) {  // b = H_t(xin) once, into the generic b region (half spectra as scratch)
+        if (d.kh > 0) {  // b = H_t(xin) once, into the generic b region
             float* bb = at<float>(ws, Lo.b);
-            if (int e = gapply<float>(xin, bb, spec[0], Lo, ws, d, 1, s)) return e;
+            // on the mixed transforms: row r2c, the column pass with the PSF multiplier, row c2r (HD: three
+            // fast launches in place of the generic transforms' ~1 ms); A/B knob ADMM_MIXED_BGEN=1: the
+            // generic transforms (half spectra as scratch)
+            if (env_int("ADMM_MIXED_BGEN", 0)) {
+                if (int e = gapply<float>(xin, bb, spec[0], Lo, ws, d, 1, s)) return e;
+            } else {
+                if (int e = hchk(admm_mixed::r2c(N, xin, spec[0], twW, rows, s), "k_row_r2c_m")) return e;
+                if (int e = hchk(admm_mixed::pass_b_cm(H, spec[0], at<cf>(ws, Lo.mM), twH, N, P, s), "k_pass_b_m<cm>"))
+                    return e;
+                if (int e = hchk(admm_mixed::c2r(N, spec[0], bb, twW, rows, s), "k_row_c2r_m")) return e;
+            }
             bimg = bb;
         }
         if (int e = hchk(admm_mixed::r2c(N, bimg, spec[0], twW, rows, s), "k_row_r2c_m")) return e;  // r_1 = b

@@ -269,6 +269,37 @@ hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long 
     });
 }
 
+hipError_t pass_b_cm(int H, cf* spec, const cf* mM, const cf* twH, int N, long long P, hipStream_t s) {
+    return with_col(H, [&](auto h) {
+        constexpr int HH = decltype(h)::value;
+        auto go = [&](auto cc) {
+            constexpr int CC = decltype(cc)::value;
+            using G = MColG<HH, CC>;
+            const int colblocks = N / CC;
+            if (hipError_t e = lds(k_pass_b_m<HH, CC, true>, G::lds_bytes())) return e;
+            hipLaunchKernelGGL((k_pass_b_m<HH, CC, true>), dim3((unsigned)(P * colblocks)), dim3(G::NT), G::lds_bytes(),
+                               s, spec, nullptr, twH, N, colblocks, 1, 0, mM);
+            return hipGetLastError();
+        };
+        constexpr int C0 = MCol<HH>::C;
+        if (N % C0 == 0) return go(std::integral_constant<int, C0>{});
+        if constexpr (C0 > 4) {
+            if (N % 4 == 0) return go(std::integral_constant<int, 4>{});
+        }
+        if constexpr (C0 > 2) {
+            if (N % 2 == 0) return go(std::integral_constant<int, 2>{});
+        }
+        return hipErrorInvalidValue;
+    });
+}
+
+hipError_t mt_mixed(const cf* mT, cf* mM, int H, int N, hipStream_t s) {
+    const long long n = (long long)H * (N + 1);
+    hipLaunchKernelGGL(k_mt_mixed, dim3((unsigned)std::min<long long>(4096, (n + 255) / 256)), dim3(256), 0, s, mT, mM,
+                       H, N);
+    return hipGetLastError();
+}
+
 hipError_t fc_mixed(const float* fcT, float* fcM, int H, int N, hipStream_t s) {
     const long long n = (long long)H * (2 * N + 1);
     const int C = pass_b_cols(H, N);

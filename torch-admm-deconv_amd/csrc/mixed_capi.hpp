@@ -30,5 +30,9 @@ hipError_t bwd_iso_q(int N, const admm::BwdIsoArgs& a, bool lastk, hipStream_t s
 hipError_t pass_b(int H, cf* spec, const float* fcM, const cf* twH, int N, long long P, hipStream_t s);
 // fcM: [H][N + 1] then the column-block-packed copy [N / C][H][C] (C = pass_b_cols): H (2N + 1) floats
 hipError_t fc_mixed(const float* fcT, float* fcM, int H, int N, hipStream_t s);
+// b = H_t(xin) on the mixed transforms: the column pass with the complex PSF multiplier mM ([H][N + 1],
+// mt_mixed of the generic path's mT [N + 1][H], halved for the packed row transforms)
+hipError_t pass_b_cm(int H, cf* spec, const cf* mM, const cf* twH, int N, long long P, hipStream_t s);
+hipError_t mt_mixed(const cf* mT, cf* mM, int H, int N, hipStream_t s);
 
 }  // namespace admm_mixed

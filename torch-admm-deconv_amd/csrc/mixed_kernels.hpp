@@ -563,6 +563,17 @@ static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restri
     }
 }
 
+// the PSF multiplier for the mixed column pass: mM[ky][kx] = mT[kx][ky] / 2 (kx in [0, N]; the / 2 as for
+// k_fc_mixed)
+static __global__ void k_mt_mixed(const cf* __restrict__ mT, cf* __restrict__ mM, int H, int N) {
+    const long long n = (long long)H * (N + 1);
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const int ky = (int)(i / (N + 1)), kx = (int)(i % (N + 1));
+        const cf v = mT[(size_t)kx * H + ky];
+        mM[i] = mkc(0.5f * v.x, 0.5f * v.y);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // pass B: column FFT -> Wiener factor -> column IFFT, in place, C columns per block
 // ---------------------------------------------------------------------------------------------
@@ -570,10 +581,14 @@ static __global__ void k_fc_mixed(const float* __restrict__ fcT, float* __restri
 // block with the next plane streamed into LDS (global_load_lds) during the inverse transform and
 // LDS-only barriers -- HD pass B 0.258-0.267 ms against 0.160 for one tile per block; an occupancy
 // target for the smooth column plans (capped registers spill and lose 4-21 %).
-template <int H, int CC>
+// CM: a complex multiplier instead of the real Wiener factor -- b = H_t(xin) once per solve (the PSF
+// multiplier mT, pre-halved and row-major: mM[ky][kx], kx in [0, N]; k_mt_mixed), in place of the generic
+// transforms' three launches.  The packed (DC, Nyquist) column then takes complex a, b (as the
+// power-of-two pass B's MODE 1).
+template <int H, int CC, bool CM = false>
 __global__ void __launch_bounds__((MColG<H, CC>::NT))
 k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g, int N, int colblocks, int order,
-           int fpack) {
+           int fpack, const cf* __restrict__ mM = nullptr) {
     using G = MColG<H, CC>;
     constexpr int Lc = G::Lc, Ec = G::Ec, C = G::C, EM = G::EM, NBz = G::NBz, Qz = G::Qz;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -593,18 +608,22 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
 #pragma unroll
     for (int j = 0; j < Ec; ++j) v[j] = bload_cf(rs, voff, j * sstep);
     // frequencies in layout(Rz): v[q + Qz k] <-> ky = t + Lc q + NBz k (valid for t + Lc q < NBz)
-    float m[EM];
+    typename std::conditional<CM, cf, float>::type m[EM];
     // the factors of this thread's column: from the column-block-packed copy (k_fc_mixed) or the
-    // row-major table
-    const float* fcP = fcM + (size_t)H * (N + 1) + (size_t)cb * H * C + c;
+    // row-major table (CM: the row-major complex multiplier)
+    const float* fcP = CM ? nullptr : fcM + (size_t)H * (N + 1) + (size_t)cb * H * C + c;
     auto load_m = [&]() {
 #pragma unroll
         for (int q = 0; q < Qz; ++q) {
             const int vt = t + Lc * q;
 #pragma unroll
-            for (int k = 0; k < G::Rz; ++k)
-                m[q + Qz * k] = (vt < NBz) ? (fpack ? fcP[(size_t)(vt + NBz * k) * C]
-                                                    : fcM[(size_t)(vt + NBz * k) * (N + 1) + col]) : 0.f;
+            for (int k = 0; k < G::Rz; ++k) {
+                if constexpr (CM)
+                    m[q + Qz * k] = (vt < NBz) ? mM[(size_t)(vt + NBz * k) * (N + 1) + col] : mkc(0.f, 0.f);
+                else
+                    m[q + Qz * k] = (vt < NBz) ? (fpack ? fcP[(size_t)(vt + NBz * k) * C]
+                                                        : fcM[(size_t)(vt + NBz * k) * (N + 1) + col]) : 0.f;
+            }
         }
     };
     __syncthreads();  // twiddles in LDS
@@ -632,10 +651,17 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
                     for (int k = 0; k < G::Rz; ++k) {
                         const int ky = vt + NBz * k;
                         const cf qv = cconj(buf.at(ky == 0 ? 0 : H - ky));
-                        const float f0 = m[q + Qz * k], fn = fcM[(size_t)ky * (N + 1) + N];
-                        const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
                         const cf x = v[q + Qz * k];
-                        v[q + Qz * k] = mkc(fmaf(a, x.x, b * qv.x), fmaf(a, x.y, b * qv.y));
+                        if constexpr (CM) {
+                            const cf m0 = m[q + Qz * k], mn = mM[(size_t)ky * (N + 1) + N];
+                            const cf a = mkc(0.5f * (m0.x + mn.x), 0.5f * (m0.y + mn.y));
+                            const cf b = mkc(0.5f * (m0.x - mn.x), 0.5f * (m0.y - mn.y));
+                            v[q + Qz * k] = cadd(cmul(x, a), cmul(qv, b));
+                        } else {
+                            const float f0 = m[q + Qz * k], fn = fcM[(size_t)ky * (N + 1) + N];
+                            const float a = 0.5f * (f0 + fn), b = 0.5f * (f0 - fn);
+                            v[q + Qz * k] = mkc(fmaf(a, x.x, b * qv.x), fmaf(a, x.y, b * qv.y));
+                        }
                     }
                 }
             }
@@ -644,7 +670,10 @@ k_pass_b_m(cf* spec, const float* __restrict__ fcM, const cf* __restrict__ twH_g
     }
     if (col != 0) {
 #pragma unroll
-        for (int i = 0; i < Qz * G::Rz; ++i) v[i] = cscale(v[i], m[i]);
+        for (int i = 0; i < Qz * G::Rz; ++i) {
+            if constexpr (CM) v[i] = cmul(v[i], m[i]);
+            else v[i] = cscale(v[i], m[i]);
+        }
     }
     mfft<H, Lc, EM, +1, 1, 1>(v, buf, tw, t, typename MCol<H>::Inv{});
 #pragma unroll
