@@ -66,7 +66,9 @@ def _c4_worker(rank, world, port, q):
         same = torch.equal(out, single)
         planes = None
         if rank in (0, world - 1):
-            planes = [(b, c, x[b, c].cpu().clone(), out[b, c].cpu().clone()) for b, c in C4_PLANES]
+            # numpy arrays travel by value: torch CPU tensors on a queue are shared through a file
+            # descriptor server in this process, gone if it exits before the parent reads (r06e)
+            planes = [(b, c, x[b, c].cpu().numpy().copy(), out[b, c].cpu().numpy().copy()) for b, c in C4_PLANES]
         del x, out, single
         torch.cuda.empty_cache()
         q.put((rank, same, planes))
@@ -97,6 +99,7 @@ def test_c4_full_size_world8_gloo(cuda_dev):
     psf = make_psf("gauss:3", 21).double()
     for r in (0, world - 1):
         for b, c, xin, got in res[r][1]:
+            xin, got = torch.from_numpy(xin), torch.from_numpy(got)
             ref = solve_fourier(xin.double().reshape(1, 1, 1024, 1024), 0.01, 0.02, psf, False, 50)
             e = rel_l2(got.reshape(1, 1, 1024, 1024), ref)
             print(f"C4 rank {r} plane ({b},{c}): rel-L2 vs fp64 oracle {e:.3e}")
