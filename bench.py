@@ -32,6 +32,21 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32-input MFMA peak (v_mfma_f32_16x16x4_f32, MI355X_MICROARCH.md)
+
+
+def mm_col_flops(H, Wh, P):
+    """Matrix-core flops per launch of the generic column pass (csrc/gcol_mm.hpp) for columns H = S * R
+    (R odd in [17, 127], the largest such factor with S <= 8): per column sequence of R complex values,
+    forward and inverse, the cosine and sine products of the (h+1)-point real matrices (h = (R-1)/2),
+    padded to 16-row tiles and 4-deep k-steps, on the real and imaginary parts; None without such a plan."""
+    Rs = [r for r in range(127, 16, -2) if H % r == 0 and H // r <= 8]
+    if not Rs:
+        return None
+    R = Rs[0]
+    S, h = H // R, (R - 1) // 2
+    M, K = -(-(h + 1) // 16) * 16, -(-(h + 1) // 4) * 4
+    return P * Wh * S * (2 * 2 * 2 * M * K * 2)
 
 CONFIGS = {
     # name: (B, C, H, W, psf kind, k, maxit, iso, description)
@@ -230,6 +245,12 @@ def generic_extras(dev, no_parity, keys=("bsd", "hd")):
             gbs = b / (t / 1e3) / 1e9 if t > 0 else None
             per[name] = {"avg_launch_ms": t / max(n, 1), "launches": n, "algorithmic_bytes_per_launch": b / max(n, 1),
                          "GBps": gbs, "frac": gbs / HBM_PEAK_GBS if gbs else None}
+        mm = mm_col_flops(H, W // 2 + 1, B * C) if e["path"] == "fused odd-length" else None
+        if mm and per["pass_b"]["avg_launch_ms"] > 0:
+            # the matrix-core column pass's own bound: its R-point DFT products on the f32 MFMA
+            tf = mm / (per["pass_b"]["avg_launch_ms"] / 1e3) / 1e12
+            per["pass_b"]["mfma"] = {"flops_per_launch": mm, "TFLOPs": tf, "peak": MFMA_F32_PEAK_TFLOPS,
+                                     "frac": tf / MFMA_F32_PEAK_TFLOPS}
         e["roofline_one_stream"] = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "per_kernel": per,
                                     "timing": "HIP events, 2 solves on one stream after the timed solves"}
         out[key] = e

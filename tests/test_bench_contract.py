@@ -113,3 +113,10 @@ def test_rocfft_rank_cache(monkeypatch):
     monkeypatch.setenv("ROCFFT_RTC_CACHE_PATH", "/somewhere/mine.db")
     bench.rocfft_rank_cache(5)
     assert os.environ["ROCFFT_RTC_CACHE_PATH"] == "/somewhere/mine.db"
+
+
+def test_mm_col_flops_plan():
+    # BSD columns 321 = 3 * 107: h = 53 -> 64-row tiles, 56-deep k; forward + inverse, cos + sin, re + im
+    import bench
+    assert bench.mm_col_flops(321, 241, 96) == 96 * 241 * 3 * (2 * 2 * 2 * 64 * 56 * 2)
+    assert bench.mm_col_flops(1024, 513, 1) is None  # no odd factor in [17, 127]
